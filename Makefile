@@ -1,0 +1,45 @@
+# Build of the MI355X volumetric path tracer (gfx950 only).
+#   make            -> cudavolumerenderer_amd/libcvr.so + cudavolumerenderer_amd/cvr (CLI)
+#   make oracle     -> oracle/liboracle.so (test infrastructure)
+# -ffp-contract=off: the kernels must perform exactly the IEEE operations of
+# the source (see include/cvr_detmath.h); the correctly-rounded fp32 divide /
+# sqrt flag is the hipcc default, spelled out because parity depends on it.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := cudavolumerenderer_amd
+CSRC := $(PKG)/csrc
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(CSRC) -Wall -Wno-unused-function
+OBJDIR := build/obj
+SRCS_HIP := $(CSRC)/cvr_kernels.hip $(CSRC)/cvr_wavefront.hip
+SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp
+OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
+HDRS := include/cvr.h include/cvr_detmath.h $(wildcard $(CSRC)/*.h)
+
+all: $(PKG)/libcvr.so $(PKG)/cvr oracle
+
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(PKG)/libcvr.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-soname,libcvr.so
+
+$(PKG)/cvr: $(CSRC)/cvr_main.cpp $(PKG)/libcvr.so include/cvr.h
+	g++ -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lcvr -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+resource-usage:
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $(CSRC)/cvr_kernels.hip -o /dev/null
+
+clean:
+	rm -rf build $(PKG)/libcvr.so $(PKG)/cvr
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean resource-usage

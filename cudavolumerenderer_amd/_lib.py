@@ -1,0 +1,376 @@
+"""ctypes binding of libcvr.so (include/cvr.h).
+
+This is the only way Python reaches the renderer: every call goes through the
+C ABI that a C/C++/Go/Java host would bind.  There is no
+Python or CPU fallback: if libcvr.so is missing or a HIP call fails, the call
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcvr.so")
+
+CVR_OK = 0
+ERRORS = {-1: "CVR_ERR_INVALID", -2: "CVR_ERR_HIP", -3: "CVR_ERR_STATE", -4: "CVR_ERR_IO",
+          -5: "CVR_ERR_UNSUPPORTED", -6: "CVR_ERR_NOMEM"}
+
+# Config::Kernel order (Config.h:87-95)
+KERNELS = ["naiveSK", "naiveMK", "regenerationSK", "streamingMK", "streamingSK", "sortingSK"]
+NAIVE_SK, NAIVE_MK, REGENERATION_SK, STREAMING_MK, STREAMING_SK, SORTING_SK = range(6)
+SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4}
+
+OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
+OPT_SCHEDULER, OPT_POOL, OPT_TIMING = 6, 7, 8
+
+
+class CvrError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class MediumDesc(C.Structure):
+    _fields_ = [("res", C.c_uint32 * 3), ("density", C.POINTER(C.c_float)),
+                ("albedo", C.POINTER(C.c_float)), ("box_min", C.c_float * 3),
+                ("box_max", C.c_float * 3), ("scale", C.c_float), ("max_density", C.c_float),
+                ("g", C.c_float), ("roughness", C.c_float * 2), ("eta", C.c_float)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("steps", C.c_uint64),
+                ("density", C.c_uint64), ("albedo", C.c_uint64), ("escaped", C.c_uint64),
+                ("truncated", C.c_uint64), ("kernel_ms", C.c_double), ("iterations", C.c_uint64),
+                ("track_ms", C.c_double), ("events_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class PathRecord(C.Structure):
+    _fields_ = [("image_id", C.c_uint32), ("flags", C.c_uint32), ("T", C.c_float * 3),
+                ("n_segments", C.c_uint32), ("n_steps", C.c_uint32), ("n_density", C.c_uint32),
+                ("n_albedo", C.c_uint32)]
+
+
+PATH_RECORD_DTYPE = np.dtype([("image_id", "<u4"), ("flags", "<u4"), ("T", "<f4", (3,)),
+                              ("n_segments", "<u4"), ("n_steps", "<u4"), ("n_density", "<u4"),
+                              ("n_albedo", "<u4")])
+assert PATH_RECORD_DTYPE.itemsize == C.sizeof(PathRecord)
+
+
+class RenderDesc(C.Structure):
+    _fields_ = [("resolution", C.c_uint32 * 2), ("n_tiles", C.c_uint32 * 2), ("iterations", C.c_uint32)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libcvr.so (built by `make` / __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    P, U32, U64, I32, I64, F = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_int64, C.c_float
+    FP = C.POINTER(C.c_float)
+    sig = {
+        "cvr_abi_version": (I32, []),
+        "cvr_create": (I32, [I32, I32, C.POINTER(P)]),
+        "cvr_destroy": (I32, [P]),
+        "cvr_last_error": (C.c_char_p, [P]),
+        "cvr_set_medium": (I32, [P, C.POINTER(MediumDesc)]),
+        "cvr_set_camera": (I32, [P, FP, FP, FP]),
+        "cvr_set_resolution": (I32, [P, U32, U32]),
+        "cvr_set_offset": (I32, [P, U32, U32]),
+        "cvr_set_iterations": (I32, [P, U32]),
+        "cvr_set_path_range": (I32, [P, U64, U64]),
+        "cvr_set_seed": (I32, [P, U32]),
+        "cvr_get_seed": (I32, [P, C.POINTER(U32)]),
+        "cvr_set_output": (I32, [P, P]),
+        "cvr_output_ptr": (P, [P]),
+        "cvr_set_stream": (I32, [P, P]),
+        "cvr_own_stream": (P, [P]),
+        "cvr_set_option": (I32, [P, I32, I64]),
+        "cvr_init": (I32, [P]),
+        "cvr_launch_render": (I32, [P]),
+        "cvr_reset": (I32, [P]),
+        "cvr_synchronize": (I32, [P]),
+        "cvr_clear_output": (I32, [P]),
+        "cvr_get_stats": (I32, [P, C.POINTER(Stats)]),
+        "cvr_copy_output": (I32, [P, FP, F]),
+        "cvr_trace_paths": (I32, [P, U32, U32, C.POINTER(PathRecord)]),
+        "cvr_device_info": (I32, [P, C.POINTER(I32), C.POINTER(I32)]),
+        "cvr_render_image": (I32, [P, C.POINTER(RenderDesc), P, FP, C.POINTER(Stats)]),
+        "cvr_default_camera": (I32, [U32, U32, FP, FP]),
+        "cvr_tiling": (I32, [U32, U32, U32, U32, C.POINTER(U32)]),
+        "cvr_tile_origin": (I32, [U32, U32, C.POINTER(U32), C.POINTER(U32)]),
+        "cvr_scene_load": (I32, [C.c_char_p, I32, C.POINTER(P)]),
+        "cvr_scene_synthetic": (I32, [C.c_char_p, U32, C.POINTER(U32), C.POINTER(P)]),
+        "cvr_scene_medium": (I32, [P, C.POINTER(MediumDesc)]),
+        "cvr_scene_raw_bytes": (I32, [P, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_size_t)]),
+        "cvr_scene_destroy": (None, [P]),
+        "cvr_write_hdr": (I32, [C.c_char_p, FP, U32, U32]),
+        "cvr_kernel_from_name": (I32, [C.c_char_p]),
+        "cvr_kernel_name": (C.c_char_p, [I32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _check(code: int, ctx=None):
+    if code != CVR_OK:
+        msg = load().cvr_last_error(ctx)
+        raise CvrError(code, msg.decode() if msg else "")
+
+
+# ------------------------------------------------------------------ helpers --
+def default_camera(width: int, height: int):
+    """Camera.h:25-71 + CudaVolPath.cpp:67-85 -> (inv_view[12], raster_to_view[2])."""
+    lib = load()
+    iv = np.zeros(12, np.float32)
+    r2v = np.zeros(2, np.float32)
+    _check(lib.cvr_default_camera(width, height, _fp(iv), _fp(r2v)))
+    return iv, r2v
+
+
+def tiling(width: int, height: int, ntx: int, nty: int):
+    lib = load()
+    td = (C.c_uint32 * 2)()
+    _check(lib.cvr_tiling(width, height, ntx, nty, td))
+    return int(td[0]), int(td[1])
+
+
+def tile_origin(tile_id: int, ntx: int, tile_dim: Sequence[int]):
+    lib = load()
+    td = (C.c_uint32 * 2)(*tile_dim)
+    org = (C.c_uint32 * 2)()
+    _check(lib.cvr_tile_origin(tile_id, ntx, td, org))
+    return int(org[0]), int(org[1])
+
+
+def write_hdr(path: str, rgba: np.ndarray):
+    rgba = np.ascontiguousarray(rgba, dtype=np.float32)
+    h, w = rgba.shape[:2]
+    _check(load().cvr_write_hdr(path.encode(), _fp(rgba), w, h))
+
+
+# ------------------------------------------------------------------- scenes --
+class Scene:
+    """A loaded or synthetic scene (SceneBuilder + Scene, Scene.h:56-81)."""
+
+    def __init__(self, handle):
+        self._h = handle
+        self.medium = MediumDesc()
+        _check(load().cvr_scene_medium(self._h, C.byref(self.medium)))
+
+    @classmethod
+    def synthetic(cls, name: str, seed: int = 0, dims: Optional[Sequence[int]] = None) -> "Scene":
+        lib = load()
+        h = C.c_void_p()
+        d = (C.c_uint32 * 3)(*dims) if dims is not None else None
+        _check(lib.cvr_scene_synthetic(name.encode(), seed, d, C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def load(cls, path: str, scene_type: str = "Auto") -> "Scene":
+        lib = load()
+        h = C.c_void_p()
+        _check(lib.cvr_scene_load(path.encode(), SCENE_TYPES[scene_type], C.byref(h)))
+        return cls(h)
+
+    @property
+    def dims(self):
+        return tuple(int(v) for v in self.medium.res)
+
+    @property
+    def density(self) -> np.ndarray:
+        """(z, y, x) view of the fp32 density grid (owned by the scene)."""
+        nx, ny, nz = self.dims
+        return np.ctypeslib.as_array(self.medium.density, shape=(nz, ny, nx))
+
+    @property
+    def albedo(self) -> np.ndarray:
+        nx, ny, nz = self.dims
+        return np.ctypeslib.as_array(self.medium.albedo, shape=(nz, ny, nx, 4))
+
+    @property
+    def raw_bytes(self) -> bytes:
+        p = C.POINTER(C.c_uint8)()
+        n = C.c_size_t()
+        _check(load().cvr_scene_raw_bytes(self._h, C.byref(p), C.byref(n)))
+        return bytes(np.ctypeslib.as_array(p, shape=(n.value,))) if n.value else b""
+
+    def close(self):
+        if self._h:
+            load().cvr_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def medium_from_arrays(density: np.ndarray, albedo: np.ndarray, box_min=(-0.5,) * 3, box_max=(0.5,) * 3,
+                       scale=100.0, max_density=None, g=0.0, roughness=(0.1, 0.1), eta=None):
+    """Build a MediumDesc over caller arrays (kept alive by the returned tuple)."""
+    density = np.ascontiguousarray(density, dtype=np.float32)
+    albedo = np.ascontiguousarray(albedo, dtype=np.float32)
+    nz, ny, nx = density.shape
+    assert albedo.shape == (nz, ny, nx, 4)
+    m = MediumDesc()
+    m.res[:] = (nx, ny, nz)
+    m.density = _fp(density)
+    m.albedo = _fp(albedo)
+    m.box_min[:] = box_min
+    m.box_max[:] = box_max
+    m.scale = scale
+    m.max_density = float(density.max()) if max_density is None else max_density
+    m.g = g
+    m.roughness[:] = roughness
+    m.eta = np.float32(np.float32(1.05) / np.float32(1.01)) if eta is None else eta
+    return m, (density, albedo)
+
+
+# ------------------------------------------------------------------ context --
+class Context:
+    """One kernel launcher bound to one GPU (VolPTKernelLauncher, RenderKernelLauncher.h:54-73)."""
+
+    def __init__(self, device: int = 0, kernel="regenerationSK"):
+        lib = load()
+        kid = KERNELS.index(kernel) if isinstance(kernel, str) else int(kernel)
+        h = C.c_void_p()
+        _check(lib.cvr_create(device, kid, C.byref(h)))
+        self._h = h
+        self.kernel = kid
+
+    def _c(self, code):
+        _check(code, self._h)
+
+    def set_medium(self, medium: MediumDesc):
+        self._c(load().cvr_set_medium(self._h, C.byref(medium)))
+
+    def set_camera(self, inv_view, raster_to_view, full_res):
+        iv = np.ascontiguousarray(inv_view, np.float32)
+        r = np.ascontiguousarray(raster_to_view, np.float32)
+        fr = np.ascontiguousarray(full_res, np.float32)
+        self._c(load().cvr_set_camera(self._h, _fp(iv), _fp(r), _fp(fr)))
+
+    def set_resolution(self, w, h):
+        self._c(load().cvr_set_resolution(self._h, w, h))
+
+    def set_offset(self, x, y):
+        self._c(load().cvr_set_offset(self._h, x, y))
+
+    def set_iterations(self, it):
+        self._c(load().cvr_set_iterations(self._h, it))
+
+    def set_path_range(self, first, count):
+        self._c(load().cvr_set_path_range(self._h, first, count))
+
+    def set_seed(self, seed):
+        self._c(load().cvr_set_seed(self._h, seed))
+
+    def get_seed(self) -> int:
+        v = C.c_uint32()
+        self._c(load().cvr_get_seed(self._h, C.byref(v)))
+        return v.value
+
+    def set_output(self, device_ptr: Optional[int]):
+        self._c(load().cvr_set_output(self._h, C.c_void_p(device_ptr) if device_ptr else None))
+
+    def output_ptr(self) -> int:
+        return load().cvr_output_ptr(self._h) or 0
+
+    def set_stream(self, stream_ptr: Optional[int]):
+        """Launch on `stream_ptr` (a hipStream_t; 0/None = the null stream)."""
+        self._c(load().cvr_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def use_own_stream(self):
+        self._c(load().cvr_set_stream(self._h, load().cvr_own_stream(self._h)))
+
+    def set_option(self, opt: int, value: int):
+        self._c(load().cvr_set_option(self._h, opt, value))
+
+    def init(self):
+        self._c(load().cvr_init(self._h))
+
+    def launch_render(self):
+        self._c(load().cvr_launch_render(self._h))
+
+    def reset(self):
+        self._c(load().cvr_reset(self._h))
+
+    def synchronize(self):
+        self._c(load().cvr_synchronize(self._h))
+
+    def clear_output(self):
+        self._c(load().cvr_clear_output(self._h))
+
+    def stats(self) -> Stats:
+        s = Stats()
+        self._c(load().cvr_get_stats(self._h, C.byref(s)))
+        return s
+
+    def copy_output(self, w, h, scale=1.0) -> np.ndarray:
+        out = np.zeros((h, w, 4), np.float32)
+        self._c(load().cvr_copy_output(self._h, _fp(out), scale))
+        return out
+
+    def trace_paths(self, first: int, count: int) -> np.ndarray:
+        out = np.zeros(count, PATH_RECORD_DTYPE)
+        self._c(load().cvr_trace_paths(self._h, first, count,
+                                       out.ctypes.data_as(C.POINTER(PathRecord))))
+        return out
+
+    def device_info(self):
+        cu, grid = C.c_int(), C.c_int()
+        self._c(load().cvr_device_info(self._h, C.byref(cu), C.byref(grid)))
+        return cu.value, grid.value
+
+    def render_image(self, width, height, n_tiles=(1, 1), iterations=20, device_image: Optional[int] = None,
+                     host: bool = True):
+        d = RenderDesc()
+        d.resolution[:] = (width, height)
+        d.n_tiles[:] = n_tiles
+        d.iterations = iterations
+        st = Stats()
+        img = np.zeros((height, width, 4), np.float32) if host else None
+        self._c(load().cvr_render_image(self._h, C.byref(d),
+                                        C.c_void_p(device_image) if device_image else None,
+                                        _fp(img) if host else None, C.byref(st)))
+        return img, st
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().cvr_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

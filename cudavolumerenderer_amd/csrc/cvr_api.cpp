@@ -1,0 +1,764 @@
+// cvr_api.cpp - C ABI implementation: contexts (kernel launchers), device
+// volume upload, the CudaVolPath tile loop, camera/tiling helpers.
+//
+// Reference map:
+//   RenderKernelLauncher / VolPTKernelLauncher  RenderKernelLauncher.h:20-174,
+//                                                RenderKernelLauncher.cu:86-361
+//   CudaVolPath::render / runIterations / getImage / prepareForNextIterations
+//                                                CudaVolPath.cpp:189-347
+//   Camera + initCamera                          Camera.h:25-71, CudaVolPath.cpp:67-85
+//   TilingConfig + initTileArray                 Config.h:61-78, CudaVolPath.cpp:13-29
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cvr.h"
+#include "cvr_kernels.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_err(std::string* dst, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  if (dst) *dst = buf;
+  return code;
+}
+
+}  // namespace
+
+struct cvr_ctx {
+  int device = 0;
+  int kernel = CVR_KERNEL_REGENERATION_SK;
+  std::string err;
+
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  bool timed = false;
+
+  // medium in HBM
+  float* d_density = nullptr;
+  float4* d_albedo = nullptr;
+  size_t n_voxels = 0;
+  bool have_medium = false;
+  cvr::MediumParams m{};
+
+  // launcher state (the reference's __constant__ symbols)
+  float inv_view[12] = {1, 0, 0, 0, 0, -1, 0, 0, 0, 0, -1, 100};
+  float r2v[2] = {0, 0};
+  float full_res[2] = {0, 0};
+  bool have_camera = false;
+  uint32_t tile_w = 0, tile_h = 0;
+  uint32_t off[2] = {0, 0};
+  uint32_t iterations = 1;
+  uint64_t n_paths = 0;
+  uint64_t range_first = 0, range_count = UINT64_MAX;
+  uint32_t seed = 0;
+
+  float4* d_out_owned = nullptr;
+  size_t out_owned_px = 0;
+  float4* d_out = nullptr;  // active output (owned or external)
+  bool external_out = false;
+
+  unsigned char* d_work = nullptr;  // queue head + stats counters
+
+  // options
+  uint32_t max_segments = 1u << 20;
+  uint32_t chunk = 128;
+  uint32_t ev_thresh = 16;
+  uint32_t grid_override = 0;
+  int scatter_eps = -1;
+
+  int cu_count = 0;
+  int persistent_grid = 0;
+  int track_grid = 0;
+  bool inited = false;
+  int scheduler = 0;  // 0 wavefront (default), 1 single persistent kernel
+
+  // wavefront pool (cvr_wavefront.hip)
+  unsigned char* d_pool = nullptr;
+  size_t pool_bytes = 0;
+  uint32_t pool_cap = 0;  // slots the allocation holds
+  uint32_t pool_max = 1u << 21;
+  cvr::WfPool pool{};
+  unsigned int* h_alive = nullptr;  // pinned ring of per-iteration flags
+  std::vector<hipEvent_t> it_events;
+  uint64_t last_iterations = 0;
+  double last_track_ms = 0, last_events_ms = 0;
+  bool wf_timing = false;
+
+  cvr_stats last{};
+};
+
+#define HIP_TRY(ctx, expr)                                                                              \
+  do {                                                                                                  \
+    hipError_t e_ = (expr);                                                                             \
+    if (e_ != hipSuccess)                                                                               \
+      return set_err((ctx) ? &(ctx)->err : nullptr, CVR_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+bool kernel_supported(int k) { return k == CVR_KERNEL_NAIVE_SK || k == CVR_KERNEL_REGENERATION_SK; }
+
+// Scatter origin offset per scheduler: every kernel subtracts
+// d*eps at a real collision except single-thread regeneration
+// (RegenerationVolPTsk_kernel.cuh:212).
+bool scatter_eps_for(const cvr_ctx* c) {
+  if (c->scatter_eps >= 0) return c->scatter_eps != 0;
+  return c->kernel != CVR_KERNEL_REGENERATION_SK;
+}
+
+int ensure_device(cvr_ctx* c) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  return CVR_OK;
+}
+
+int ensure_output(cvr_ctx* c) {
+  if (c->external_out) return CVR_OK;
+  const size_t px = (size_t)c->tile_w * c->tile_h;
+  if (px == 0) return set_err(&c->err, CVR_ERR_STATE, "resolution not set");
+  if (c->out_owned_px < px) {
+    if (c->d_out_owned) (void)hipFree(c->d_out_owned);
+    c->d_out_owned = nullptr;
+    HIP_TRY(c, hipMalloc(&c->d_out_owned, px * sizeof(float4)));
+    HIP_TRY(c, hipMemsetAsync(c->d_out_owned, 0, px * sizeof(float4), c->stream));
+    c->out_owned_px = px;
+  }
+  c->d_out = c->d_out_owned;
+  return CVR_OK;
+}
+
+void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_t count) {
+  memcpy(L.M, c->inv_view, sizeof(L.M));
+  L.r2v[0] = c->r2v[0];
+  L.r2v[1] = c->r2v[1];
+  L.full_res[0] = c->full_res[0];
+  L.full_res[1] = c->full_res[1];
+  L.tile_res[0] = (float)c->tile_w;  // copyResolution(make_float2(res.x, res.y))
+  L.tile_res[1] = (float)c->tile_h;
+  L.off[0] = c->off[0];
+  L.off[1] = c->off[1];
+  L.tile_px = (uint32_t)(L.tile_res[0] * L.tile_res[1]);
+  L.tile_w = (uint32_t)L.tile_res[0];
+  L.path_first = (uint32_t)first;
+  L.path_count = (uint32_t)count;
+  L.seed_base = c->seed;
+  L.max_segments = c->max_segments;
+  L.out = c->d_out;
+  L.queue = reinterpret_cast<unsigned int*>(c->d_work);
+  L.stats = reinterpret_cast<unsigned long long*>(c->d_work + 64);
+  L.chunk = c->chunk ? c->chunk : 128;
+  L.ev_thresh = c->ev_thresh ? c->ev_thresh : 1;
+}
+
+int check_ready(cvr_ctx* c) {
+  if (!c->have_medium) return set_err(&c->err, CVR_ERR_STATE, "medium not set (cvr_set_medium)");
+  if (!c->have_camera) return set_err(&c->err, CVR_ERR_STATE, "camera not set (cvr_set_camera)");
+  if (c->tile_w == 0 || c->tile_h == 0) return set_err(&c->err, CVR_ERR_STATE, "resolution not set");
+  return CVR_OK;
+}
+
+int do_init(cvr_ctx* c) {
+  if (c->inited) return CVR_OK;
+  int r = ensure_device(c);
+  if (r) return r;
+  hipDeviceProp_t prop;
+  HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
+  c->cu_count = prop.multiProcessorCount;
+  int bpc = 0;
+  HIP_TRY(c, cvr::persistent_occupancy(scatter_eps_for(c), &bpc));
+  if (bpc < 1) bpc = 1;
+  c->persistent_grid = bpc * c->cu_count;
+  int tbpc = 0;
+  HIP_TRY(c, cvr::wf_track_occupancy(&tbpc));
+  if (tbpc < 1) tbpc = 1;
+  c->track_grid = tbpc * c->cu_count;
+  c->inited = true;
+  return CVR_OK;
+}
+
+constexpr uint32_t kAliveRing = 8;
+
+// Carve the SoA pool + per-wave cursors/stat rows out of one allocation.
+int ensure_pool(cvr_ctx* c, uint32_t n) {
+  n = (n + 255u) & ~255u;
+  const uint32_t ev_waves = n / 64u;
+  const uint32_t tr_waves = (uint32_t)c->track_grid * 4u;
+  const size_t slot_bytes = 19 * sizeof(uint32_t);  // 11 floats + 6 rng + img + meta
+  const size_t need = (size_t)n * slot_bytes + (size_t)ev_waves * 8 + 256 + kAliveRing * 4 + 256 +
+                      (size_t)(ev_waves + tr_waves) * 64 + 4096;
+  if (need > c->pool_bytes) {
+    if (c->d_pool) (void)hipFree(c->d_pool);
+    c->d_pool = nullptr;
+    c->pool_bytes = 0;
+    HIP_TRY(c, hipMalloc(&c->d_pool, need));
+    c->pool_bytes = need;
+  }
+  if (!c->h_alive) HIP_TRY(c, hipHostMalloc(&c->h_alive, kAliveRing * sizeof(unsigned int), hipHostMallocDefault));
+  unsigned char* p = c->d_pool;
+  auto take = [&](size_t bytes) {
+    unsigned char* r = p;
+    p += (bytes + 255) & ~(size_t)255;
+    return r;
+  };
+  cvr::WfPool& P = c->pool;
+  float** fl[] = {&P.ox, &P.oy, &P.oz, &P.dx, &P.dy, &P.dz, &P.tx, &P.ty, &P.tz, &P.dist, &P.t};
+  for (float** f : fl) *f = reinterpret_cast<float*>(take((size_t)n * 4));
+  uint32_t** ui[] = {&P.r0, &P.r1, &P.r2, &P.r3, &P.r4, &P.rd, &P.img, &P.meta};
+  for (uint32_t** u : ui) *u = reinterpret_cast<uint32_t*>(take((size_t)n * 4));
+  P.cursor = reinterpret_cast<uint32_t*>(take((size_t)ev_waves * 8));
+  P.head = reinterpret_cast<unsigned int*>(take(256));
+  P.alive = reinterpret_cast<unsigned int*>(take(kAliveRing * 4));
+  P.stats_events = reinterpret_cast<unsigned long long*>(take((size_t)ev_waves * 64));
+  P.stats_track = reinterpret_cast<unsigned long long*>(take((size_t)tr_waves * 64));
+  P.n = n;
+  c->pool_cap = n;
+  return CVR_OK;
+}
+
+// The wavefront render of one launch: events / track alternate until no
+// slot is alive.  The host polls the alive flags every few iterations.
+int wf_render(cvr_ctx* c, const cvr::LaunchParams& L, bool eps) {
+  uint32_t n = L.path_count < c->pool_max ? L.path_count : c->pool_max;
+  if (n < 256) n = 256;
+  int r = ensure_pool(c, n);
+  if (r) return r;
+  cvr::WfPool P = c->pool;
+  const uint32_t ev_waves = P.n / 64u;
+  const uint32_t tr_waves = (uint32_t)c->track_grid * 4u;
+  hipStream_t s = c->stream;
+  HIP_TRY(c, hipMemsetAsync(P.meta, 0, (size_t)P.n * 4, s));  // WF_FREE
+  HIP_TRY(c, hipMemsetAsync(P.cursor, 0, (size_t)ev_waves * 8, s));
+  HIP_TRY(c, hipMemsetAsync(P.head, 0, 256, s));
+  HIP_TRY(c, hipMemsetAsync(P.stats_events, 0, (size_t)ev_waves * 64, s));
+  HIP_TRY(c, hipMemsetAsync(P.stats_track, 0, (size_t)tr_waves * 64, s));
+  uint32_t it = 0;
+  bool done = false;
+  if (c->wf_timing && c->it_events.empty()) {
+    c->it_events.resize(3 * 512);
+    for (auto& e : c->it_events) HIP_TRY(c, hipEventCreate(&e));
+  }
+  double track_ms = 0, events_ms = 0;
+  uint32_t timed_its = 0;
+  while (!done) {
+    cvr::WfPool Pi = P;
+    Pi.alive = P.alive + (it % kAliveRing);
+    HIP_TRY(c, hipMemsetAsync(Pi.alive, 0, 4, s));
+    const bool tm = c->wf_timing && timed_its < 512;
+    if (tm) HIP_TRY(c, hipEventRecord(c->it_events[3 * timed_its], s));
+    HIP_TRY(c, cvr::wf_launch_events(c->m, L, Pi, eps, s));
+    if (tm) HIP_TRY(c, hipEventRecord(c->it_events[3 * timed_its + 1], s));
+    HIP_TRY(c, cvr::wf_launch_track(c->m, L, Pi, (uint32_t)c->track_grid, s));
+    if (tm) {
+      HIP_TRY(c, hipEventRecord(c->it_events[3 * timed_its + 2], s));
+      ++timed_its;
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->h_alive + (it % kAliveRing), Pi.alive, 4, hipMemcpyDeviceToHost, s));
+    ++it;
+    if (it % 4 == 0) {
+      HIP_TRY(c, hipStreamSynchronize(s));
+      for (uint32_t k = it - 4; k < it; ++k)
+        if (c->h_alive[k % kAliveRing] == 0) done = true;
+    }
+    if (it > 100000) return set_err(&c->err, CVR_ERR_STATE, "wavefront render did not converge");
+  }
+  for (uint32_t k = 0; k < timed_its; ++k) {
+    float a = 0, b = 0;
+    HIP_TRY(c, hipEventElapsedTime(&a, c->it_events[3 * k], c->it_events[3 * k + 1]));
+    HIP_TRY(c, hipEventElapsedTime(&b, c->it_events[3 * k + 1], c->it_events[3 * k + 2]));
+    events_ms += a;
+    track_ms += b;
+  }
+  // fold the per-wave counters into the context's 8 stats words
+  unsigned long long* stats = reinterpret_cast<unsigned long long*>(c->d_work + 64);
+  HIP_TRY(c, cvr::wf_launch_reduce(P.stats_events, ev_waves, stats, s));
+  HIP_TRY(c, cvr::wf_launch_reduce(P.stats_track, tr_waves, stats + 8, s));
+  c->last_iterations = it;
+  c->last_track_ms = track_ms;
+  c->last_events_ms = events_ms;
+  return CVR_OK;
+}
+
+void compute_range(const cvr_ctx* c, uint64_t* first, uint64_t* count) {
+  uint64_t f = c->range_first < c->n_paths ? c->range_first : c->n_paths;
+  uint64_t n = c->n_paths - f;
+  if (c->range_count < n) n = c->range_count;
+  *first = f;
+  *count = n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int cvr_abi_version(void) { return CVR_ABI_VERSION; }
+
+const char* cvr_last_error(const cvr_ctx* ctx) {
+  if (ctx && !ctx->err.empty()) return ctx->err.c_str();
+  return g_last_error.c_str();
+}
+
+int cvr_create(int device, int kernel, cvr_ctx** out) {
+  if (!out) return set_err(nullptr, CVR_ERR_INVALID, "out is NULL");
+  *out = nullptr;
+  if (kernel < 0 || kernel >= CVR_KERNEL_UNKNOWN)
+    return set_err(nullptr, CVR_ERR_INVALID, "unknown kernel id %d", kernel);
+  if (!kernel_supported(kernel))
+    return set_err(nullptr, CVR_ERR_UNSUPPORTED, "kernel %s is not implemented yet", cvr_kernel_name(kernel));
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return set_err(nullptr, CVR_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= ndev) return set_err(nullptr, CVR_ERR_INVALID, "device %d out of range", device);
+  cvr_ctx* c = new cvr_ctx();
+  c->device = device;
+  c->kernel = kernel;
+  auto fail = [&](const char* what, hipError_t err) {
+    int r = set_err(nullptr, CVR_ERR_HIP, "%s: %s", what, hipGetErrorString(err));
+    cvr_destroy(c);
+    return r;
+  };
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail("hipSetDevice", e);
+  if ((e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail("hipStreamCreate", e);
+  c->stream = c->own_stream;
+  if ((e = hipEventCreate(&c->ev_start)) != hipSuccess) return fail("hipEventCreate", e);
+  if ((e = hipEventCreate(&c->ev_stop)) != hipSuccess) return fail("hipEventCreate", e);
+  if ((e = hipMalloc(&c->d_work, 256)) != hipSuccess) return fail("hipMalloc(work)", e);
+  // stats words: [64,128) single-kernel launches / wavefront events, [128,192) wavefront track
+  if ((e = hipMemset(c->d_work, 0, 256)) != hipSuccess) return fail("hipMemset(work)", e);
+  *out = c;
+  return CVR_OK;
+}
+
+int cvr_destroy(cvr_ctx* c) {
+  if (!c) return CVR_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->d_density) (void)hipFree(c->d_density);
+  if (c->d_albedo) (void)hipFree(c->d_albedo);
+  if (c->d_out_owned) (void)hipFree(c->d_out_owned);
+  if (c->d_work) (void)hipFree(c->d_work);
+  if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+  if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->d_pool) (void)hipFree(c->d_pool);
+  if (c->h_alive) (void)hipHostFree(c->h_alive);
+  for (auto& e : c->it_events) (void)hipEventDestroy(e);
+  delete c;
+  return CVR_OK;
+}
+
+int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
+  if (!c || !md) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (!md->density || !md->albedo) return set_err(&c->err, CVR_ERR_INVALID, "density/albedo is NULL");
+  if (md->res[0] == 0 || md->res[1] == 0 || md->res[2] == 0)
+    return set_err(&c->err, CVR_ERR_INVALID, "empty grid");
+  const size_t n = (size_t)md->res[0] * md->res[1] * md->res[2];
+  if (n > 0xFFFFFFFFull) return set_err(&c->err, CVR_ERR_INVALID, "grid exceeds 2^32 voxels");
+  int r = ensure_device(c);
+  if (r) return r;
+  if (n != c->n_voxels) {
+    if (c->d_density) (void)hipFree(c->d_density);
+    if (c->d_albedo) (void)hipFree(c->d_albedo);
+    c->d_density = nullptr;
+    c->d_albedo = nullptr;
+    HIP_TRY(c, hipMalloc(&c->d_density, n * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&c->d_albedo, n * sizeof(float4)));
+    c->n_voxels = n;
+  }
+  HIP_TRY(c, hipMemcpy(c->d_density, md->density, n * sizeof(float), hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMemcpy(c->d_albedo, md->albedo, n * sizeof(float4), hipMemcpyHostToDevice));
+  cvr::MediumParams& m = c->m;
+  m.density = c->d_density;
+  m.albedo = c->d_albedo;
+  m.rx = md->res[0];
+  m.ry = md->res[1];
+  m.rz = md->res[2];
+  m.gx = (float)(md->res[0] - 1u);
+  m.gy = (float)(md->res[1] - 1u);
+  m.gz = (float)(md->res[2] - 1u);
+  m.bmin = cvr::V3{md->box_min[0], md->box_min[1], md->box_min[2]};
+  m.bmax = cvr::V3{md->box_max[0], md->box_max[1], md->box_max[2]};
+  const float ex = md->box_max[0] - md->box_min[0], ey = md->box_max[1] - md->box_min[1],
+              ez = md->box_max[2] - md->box_min[2];
+  m.shift = cvr::V3{md->box_min[0] / ex, md->box_min[1] / ey, md->box_min[2] / ez};
+  m.scale = md->scale;
+  m.inv_sigma = 1.0f / (md->scale * md->max_density);
+  m.g = md->g;
+  m.ax = md->roughness[0];
+  m.ay = md->roughness[1];
+  m.eta = md->eta;
+  c->have_medium = true;
+  return CVR_OK;
+}
+
+int cvr_set_camera(cvr_ctx* c, const float inv_view[12], const float r2v[2], const float full_res[2]) {
+  if (!c || !inv_view || !r2v || !full_res) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  memcpy(c->inv_view, inv_view, sizeof(c->inv_view));
+  c->r2v[0] = r2v[0];
+  c->r2v[1] = r2v[1];
+  c->full_res[0] = full_res[0];
+  c->full_res[1] = full_res[1];
+  c->have_camera = true;
+  return CVR_OK;
+}
+
+int cvr_set_resolution(cvr_ctx* c, uint32_t w, uint32_t h) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  if (w == 0 || h == 0) return set_err(&c->err, CVR_ERR_INVALID, "zero tile resolution");
+  if ((uint64_t)w * h > (1ull << 24))
+    return set_err(&c->err, CVR_ERR_INVALID, "tile of %ux%u exceeds 2^24 pixels (float pixel indexing)", w, h);
+  c->tile_w = w;
+  c->tile_h = h;
+  c->n_paths = (uint64_t)w * h * c->iterations;
+  return ensure_output(c);
+}
+
+int cvr_set_offset(cvr_ctx* c, uint32_t x, uint32_t y) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  c->off[0] = x;
+  c->off[1] = y;
+  return CVR_OK;
+}
+
+int cvr_set_iterations(cvr_ctx* c, uint32_t it) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  const uint64_t np = (uint64_t)c->tile_w * c->tile_h * it;
+  if (np > 0xFFFFFFFFull)
+    return set_err(&c->err, CVR_ERR_INVALID, "n_paths = %llu exceeds the reference's uint32 path ids",
+                   (unsigned long long)np);
+  c->iterations = it;
+  c->n_paths = np;
+  return CVR_OK;
+}
+
+int cvr_set_path_range(cvr_ctx* c, uint64_t first, uint64_t count) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  c->range_first = first;
+  c->range_count = count;
+  return CVR_OK;
+}
+
+int cvr_set_seed(cvr_ctx* c, uint32_t seed) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  c->seed = seed;
+  return CVR_OK;
+}
+
+int cvr_get_seed(const cvr_ctx* c, uint32_t* seed) {
+  if (!c || !seed) return set_err(nullptr, CVR_ERR_INVALID, "NULL argument");
+  *seed = c->seed;
+  return CVR_OK;
+}
+
+int cvr_set_output(cvr_ctx* c, void* p) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  if (p) {
+    c->d_out = static_cast<float4*>(p);
+    c->external_out = true;
+    return CVR_OK;
+  }
+  c->external_out = false;
+  if (c->tile_w && c->tile_h) return ensure_output(c);
+  c->d_out = nullptr;
+  return CVR_OK;
+}
+
+void* cvr_output_ptr(cvr_ctx* c) { return c ? c->d_out : nullptr; }
+
+int cvr_set_stream(cvr_ctx* c, void* s) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  c->stream = static_cast<hipStream_t>(s);  // NULL = the device's null stream
+  return CVR_OK;
+}
+
+void* cvr_own_stream(cvr_ctx* c) { return c ? (void*)c->own_stream : nullptr; }
+
+int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  switch (opt) {
+    case CVR_OPT_MAX_SEGMENTS:
+      if (v < 0) return set_err(&c->err, CVR_ERR_INVALID, "max_segments < 0");
+      c->max_segments = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_CHUNK:
+      if (v < 1 || v > (1 << 20)) return set_err(&c->err, CVR_ERR_INVALID, "chunk out of range");
+      c->chunk = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_EVENT_THRESHOLD:
+      if (v < 1 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "event threshold must be 1..64");
+      c->ev_thresh = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_GRID:
+      if (v < 0) return set_err(&c->err, CVR_ERR_INVALID, "grid < 0");
+      c->grid_override = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_SCHEDULER:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "scheduler must be 0 or 1");
+      c->scheduler = (int)v;
+      return CVR_OK;
+    case CVR_OPT_POOL:
+      if (v < 256 || v > (1 << 26)) return set_err(&c->err, CVR_ERR_INVALID, "pool size out of range");
+      c->pool_max = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_TIMING:
+      c->wf_timing = v != 0;
+      return CVR_OK;
+    case CVR_OPT_SCATTER_EPS:
+      if (v < -1 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "scatter_eps must be -1, 0 or 1");
+      c->scatter_eps = (int)v;
+      c->inited = false;
+      return CVR_OK;
+    default:
+      return set_err(&c->err, CVR_ERR_INVALID, "unknown option %d", opt);
+  }
+}
+
+int cvr_init(cvr_ctx* c) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  return do_init(c);
+}
+
+int cvr_device_info(cvr_ctx* c, int* cu_count, int* grid) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  int r = do_init(c);
+  if (r) return r;
+  if (cu_count) *cu_count = c->cu_count;
+  if (grid) *grid = c->persistent_grid;
+  return CVR_OK;
+}
+
+int cvr_launch_render(cvr_ctx* c) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  int r = check_ready(c);
+  if (r) return r;
+  if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
+  if ((r = do_init(c))) return r;
+  uint64_t first, count;
+  compute_range(c, &first, &count);
+  cvr::LaunchParams L{};
+  fill_launch(c, L, first, count);
+  const bool eps = scatter_eps_for(c);
+  HIP_TRY(c, hipMemsetAsync(c->d_work, 0, 192, c->stream));
+  HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
+  c->last_iterations = 0;
+  c->last_track_ms = c->last_events_ms = 0;
+  if (c->kernel == CVR_KERNEL_NAIVE_SK) {
+    HIP_TRY(c, cvr::launch_naive(c->m, L, eps, c->stream));
+  } else if (c->scheduler == 1) {
+    const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
+    HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, grid, c->stream));
+  } else if (L.path_count > 0) {
+    if ((r = wf_render(c, L, eps))) return r;
+  }
+  HIP_TRY(c, hipEventRecord(c->ev_stop, c->stream));
+  c->timed = true;
+  return CVR_OK;
+}
+
+int cvr_synchronize(cvr_ctx* c) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return CVR_OK;
+}
+
+int cvr_reset(cvr_ctx* c) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // RegenerationVolPTsk::reset: head = 0 (our head is re-zeroed per launch),
+  // seed_ += n_paths.  NaiveVolPTsk::reset only synchronises.
+  if (c->kernel == CVR_KERNEL_REGENERATION_SK) c->seed += (uint32_t)c->n_paths;
+  return CVR_OK;
+}
+
+int cvr_clear_output(cvr_ctx* c) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
+  HIP_TRY(c, hipMemsetAsync(c->d_out, 0, (size_t)c->tile_w * c->tile_h * sizeof(float4), c->stream));
+  return CVR_OK;
+}
+
+int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
+  if (!c || !st) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  unsigned long long w[16] = {0};
+  HIP_TRY(c, hipMemcpy(w, c->d_work + 64, sizeof(w), hipMemcpyDeviceToHost));
+  unsigned long long v[8];
+  for (int k = 0; k < 8; ++k) v[k] = w[k] + w[8 + k];  // wavefront: events + track rows
+  cvr_stats s{};
+  s.paths = v[cvr::STAT_PATHS];
+  s.segments = v[cvr::STAT_SEGMENTS];
+  s.steps = v[cvr::STAT_STEPS];
+  s.density = v[cvr::STAT_DENSITY];
+  s.albedo = v[cvr::STAT_ALBEDO];
+  s.escaped = v[cvr::STAT_ESCAPED];
+  s.truncated = v[cvr::STAT_TRUNCATED];
+  s.kernel_ms = 0.0;
+  if (c->timed) {
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, c->ev_start, c->ev_stop));
+    s.kernel_ms = ms;
+  }
+  s.iterations = c->last_iterations;
+  s.track_ms = c->last_track_ms;
+  s.events_ms = c->last_events_ms;
+  *st = s;
+  c->last = s;
+  return CVR_OK;
+}
+
+int cvr_copy_output(cvr_ctx* c, float* host, float scale) {
+  if (!c || !host) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
+  const size_t n = (size_t)c->tile_w * c->tile_h * 4;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(host, c->d_out, n * sizeof(float), hipMemcpyDeviceToHost));
+  if (scale != 1.0f)
+    for (size_t i = 0; i < n; ++i) host[i] = host[i] / scale;
+  return CVR_OK;
+}
+
+int cvr_trace_paths(cvr_ctx* c, uint32_t first, uint32_t count, cvr_path_record* out) {
+  if (!c || !out) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  int r = check_ready(c);
+  if (r) return r;
+  if (count == 0) return CVR_OK;
+  cvr::LaunchParams L{};
+  fill_launch(c, L, first, count);
+  cvr::PathRecord* d_rec = nullptr;
+  HIP_TRY(c, hipMalloc(&d_rec, (size_t)count * sizeof(cvr::PathRecord)));
+  hipError_t e = cvr::launch_trace(c->m, L, scatter_eps_for(c), d_rec, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess)
+    e = hipMemcpy(out, d_rec, (size_t)count * sizeof(cvr::PathRecord), hipMemcpyDeviceToHost);
+  (void)hipFree(d_rec);
+  if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "trace: %s", hipGetErrorString(e));
+  return CVR_OK;
+}
+
+// ------------------------------------------------------------ renderer ----
+int cvr_render_image(cvr_ctx* c, const cvr_render_desc* d, void* device_image, float* host_image, cvr_stats* stats) {
+  if (!c || !d) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  uint32_t tile_dim[2];
+  int r = cvr_tiling(d->resolution[0], d->resolution[1], d->n_tiles[0], d->n_tiles[1], tile_dim);
+  if (r) return set_err(&c->err, r, "%s", g_last_error.c_str());
+  if ((r = cvr_set_resolution(c, tile_dim[0], tile_dim[1]))) return r;
+  if ((r = cvr_set_iterations(c, d->iterations))) return r;  // setNIterations
+  if ((r = check_ready(c))) return r;
+  const uint32_t W = d->resolution[0], H = d->resolution[1];
+  const uint32_t ntiles = d->n_tiles[0] * d->n_tiles[1];
+  float4* dimg = static_cast<float4*>(device_image);
+  float4* tmp_img = nullptr;
+  if (!dimg && host_image) {
+    HIP_TRY(c, hipMalloc(&tmp_img, (size_t)W * H * sizeof(float4)));
+    HIP_TRY(c, hipMemsetAsync(tmp_img, 0, (size_t)W * H * sizeof(float4), c->stream));
+    dimg = tmp_img;
+  }
+  cvr_stats acc{};
+  // initRenderState: memset the accumulator
+  if ((r = cvr_clear_output(c))) goto done;
+  for (uint32_t k = 0; k < ntiles; ++k) {
+    uint32_t org[2];
+    cvr_tile_origin(k, d->n_tiles[0], tile_dim, org);
+    if ((r = cvr_set_offset(c, org[0], org[1]))) goto done;  // copyOffset
+    if ((r = cvr_launch_render(c))) goto done;               // launchRender
+    if (dimg) {  // getImage: scale by 1/current_iteration_ into the image
+      hipError_t e = cvr::launch_tile_to_image(c->d_out, tile_dim[0], tile_dim[1], dimg, W, org[0], org[1],
+                                               (float)d->iterations, c->stream);
+      if (e != hipSuccess) {
+        r = set_err(&c->err, CVR_ERR_HIP, "tile transfer: %s", hipGetErrorString(e));
+        goto done;
+      }
+    }
+    cvr_stats s{};
+    if ((r = cvr_get_stats(c, &s))) goto done;  // synchronises (reset() does too)
+    acc.paths += s.paths;
+    acc.segments += s.segments;
+    acc.steps += s.steps;
+    acc.density += s.density;
+    acc.albedo += s.albedo;
+    acc.escaped += s.escaped;
+    acc.truncated += s.truncated;
+    acc.kernel_ms += s.kernel_ms;
+    if ((r = cvr_reset(c))) goto done;  // prepareForNextIterations
+    if (ntiles != 1 && (r = cvr_clear_output(c))) goto done;
+  }
+  if (host_image) {
+    hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(host_image, dimg, (size_t)W * H * sizeof(float4), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) {
+      r = set_err(&c->err, CVR_ERR_HIP, "image copy: %s", hipGetErrorString(e));
+      goto done;
+    }
+  }
+  if (stats) *stats = acc;
+done:
+  if (tmp_img) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(tmp_img);
+  }
+  return r;
+}
+
+// ------------------------------------------------------------- helpers ----
+int cvr_default_camera(uint32_t w, uint32_t h, float inv_view[12], float r2v[2]) {
+  if (!inv_view || !r2v || w == 0 || h == 0) return set_err(nullptr, CVR_ERR_INVALID, "bad camera arguments");
+  // Camera(400,400,0.7) then setResolution(w,h) -> setFovFromX(fov.x)
+  const float fov_x = 0.7f;
+  const float fov_y = ((float)h / (float)w) * fov_x;
+  r2v[0] = tanf(fov_x * CVR_PI_F / 360.f);
+  r2v[1] = tanf(fov_y * CVR_PI_F / 360.f);
+  // glm column-major model view: col0 right (1,0,0,0) [MITSUBA_COMPARABLE],
+  // col1 up (0,-1,0,0), col2 view (0,0,-1,0), col3 position (0,0,100,1);
+  // initCamera takes rows of its transpose's first three rows.
+  const float mv[16] = {1, 0, 0, 0, 0, -1, 0, 0, 0, 0, -1, 0, 0, 0, 100.0f, 1};
+  const int idx[12] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14};
+  for (int i = 0; i < 12; ++i) inv_view[i] = mv[idx[i]];
+  return CVR_OK;
+}
+
+int cvr_tiling(uint32_t w, uint32_t h, uint32_t ntx, uint32_t nty, uint32_t tile_dim[2]) {
+  if (!tile_dim || ntx == 0 || nty == 0) return set_err(nullptr, CVR_ERR_INVALID, "bad tiling arguments");
+  // tile_dim = (int)ceil(resolution / n_tiles) with integer division inside
+  // ceil: the remainder is never rendered (Q1).
+  tile_dim[0] = w / ntx;
+  tile_dim[1] = h / nty;
+  if (tile_dim[0] == 0 || tile_dim[1] == 0) return set_err(nullptr, CVR_ERR_INVALID, "more tiles than pixels");
+  return CVR_OK;
+}
+
+int cvr_tile_origin(uint32_t id, uint32_t ntx, const uint32_t tile_dim[2], uint32_t org[2]) {
+  if (!tile_dim || !org || ntx == 0) return set_err(nullptr, CVR_ERR_INVALID, "bad tile arguments");
+  org[0] = tile_dim[0] * (id % ntx);
+  org[1] = tile_dim[1] * (uint32_t)(int)((float)id / (float)ntx);
+  return CVR_OK;
+}
+
+int cvr_kernel_from_name(const char* name) {
+  static const char* names[] = {"naiveSK", "naiveMK", "regenerationSK", "streamingMK", "streamingSK", "sortingSK"};
+  if (!name) return CVR_KERNEL_UNKNOWN;
+  for (int i = 0; i < 6; ++i)
+    if (strcmp(name, names[i]) == 0) return i;
+  return CVR_KERNEL_UNKNOWN;
+}
+
+const char* cvr_kernel_name(int k) {
+  static const char* names[] = {"naiveSK", "naiveMK", "regenerationSK", "streamingMK", "streamingSK", "sortingSK"};
+  if (k < 0 || k > 5) return "unknown";
+  return names[k];
+}
+
+}  // extern "C"

@@ -1,0 +1,50 @@
+// cvr_kernels.h - host-side launch entry points of cvr_kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cvr_walk.h"
+
+namespace cvr {
+
+// Per-path debug record; layout identical to cvr_path_record (include/cvr.h)
+// and oracle_path (oracle/cvr_oracle.c).
+struct PathRecord {
+  uint32_t image_id;
+  uint32_t flags;  // bit0 escaped (contributed), bit1 truncated
+  float T[3];
+  uint32_t n_segments, n_steps, n_density, n_albedo;
+};
+
+// Ray-slot pool of the wavefront scheduler (cvr_wavefront.hip), SoA in HBM.
+struct WfPool {
+  float *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz, *dist, *t;
+  uint32_t *r0, *r1, *r2, *r3, *r4, *rd;
+  uint32_t* img;
+  uint32_t* meta;    // state | normal code << 2 | segments << 8
+  uint32_t* cursor;  // per events-wave [q_next, q_end) into the path-id range
+  unsigned int* head;  // global path-id dequeue head
+  unsigned int* alive; // set by the events kernel when a slot needs tracking
+  unsigned long long* stats_events;  // per events-wave rows of 8 counters
+  unsigned long long* stats_track;   // per track-wave rows of 8 counters
+  uint32_t n;        // slots
+};
+
+hipError_t wf_launch_events(const MediumParams& m, const LaunchParams& L, const WfPool& P, bool scatter_eps,
+                            hipStream_t s);
+hipError_t wf_launch_track(const MediumParams& m, const LaunchParams& L, const WfPool& P, uint32_t grid,
+                           hipStream_t s);
+hipError_t wf_track_occupancy(int* blocks_per_cu);
+hipError_t wf_launch_reduce(const unsigned long long* rows, uint32_t nrows, unsigned long long* out, hipStream_t s);
+
+hipError_t launch_naive(const MediumParams& m, const LaunchParams& L, bool scatter_eps, hipStream_t s);
+hipError_t launch_persistent(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
+                             hipStream_t s);
+hipError_t persistent_occupancy(bool scatter_eps, int* blocks_per_cu);
+hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatter_eps, PathRecord* rec,
+                        hipStream_t s);
+hipError_t launch_tile_to_image(const float4* tile, uint32_t tw, uint32_t th, float4* image, uint32_t iw,
+                                uint32_t ox, uint32_t oy, float scale, hipStream_t s);
+
+}  // namespace cvr

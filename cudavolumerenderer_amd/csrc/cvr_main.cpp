@@ -1,0 +1,209 @@
+// cvr_main.cpp - command-line front end with the reference's flags
+// (ConfigParser.cpp:10-165, Main.cpp:46-146), driving libcvr through its C
+// ABI only.
+//
+//   cvr [--scene-file|-s] FILE [--scene-type Auto|MitsubaXml|Vdb|Raw|Mhd]
+//       [--kernel|-k naiveSK|regenerationSK|...] [--algorithm|-a cudaVolPath]
+//       [--iterations|-i N] [--resolution|-r W [H]] [--number-of-tiles X [Y]]
+//       [--trials N] [--output|-o NAME] [--interactive BOOL]
+//       [--use-unified-memory BOOL]
+//   extensions: --synthetic bucky|manix|hetvol, --device N, --seed S
+//
+// Differences from the reference, on purpose: the timer is wall clock (the
+// reference uses clock(), i.e. CPU time, Main.cpp:51-77); main does not wait
+// for Enter; --interactive true has no GL viewer here (out of scope, SURVEY
+// §2.1) and falls back to the headless path with a notice.
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "cvr.h"
+
+namespace {
+
+struct Options {
+  std::string scene_file, scene_type = "Auto", algorithm = "cudaVolPath", kernel = "regenerationSK";
+  std::string output, synthetic;
+  bool interactive = true, unified = false;
+  unsigned trials = 1, iterations = 20, device = 0, seed = 0;
+  std::vector<unsigned> tiles{1, 1}, resolution{1024, 1024};
+};
+
+bool parse_bool(const std::string& v) { return v == "1" || v == "true" || v == "on" || v == "yes"; }
+
+void usage() {
+  printf(
+      "Generic:\n"
+      "  -h [ --help ]                      produce help message\n"
+      "  -s [ --scene-file ] arg            scene file to parse\n"
+      "  --scene-type arg (=Auto)           Auto, MitsubaXml, Vdb, Raw, Mhd\n"
+      "  --interactive arg (=1)             (no GL viewer in this build: runs headless)\n"
+      "  --trials arg (=1)                  number of times to run the algorithm\n"
+      "  -a [ --algorithm ] arg (=cudaVolPath)\n"
+      "  -k [ --kernel ] arg (=regenerationSK)\n"
+      "  --number-of-tiles arg (=1 1)\n"
+      "  --use-unified-memory arg (=0)      accepted for compatibility (288 GB HBM)\n"
+      "Scene configuration override:\n"
+      "  -i [ --iterations ] arg (=20)\n"
+      "  -o [ --output ] arg\n"
+      "  -r [ --resolution ] arg (=1024 1024)\n"
+      "Extensions:\n"
+      "  --synthetic bucky|manix|hetvol     use a built-in proxy scene\n"
+      "  --device N, --seed S\n");
+}
+
+bool is_flag(const char* a) { return a[0] == '-' && !(a[1] >= '0' && a[1] <= '9'); }
+
+int parse(int argc, char** argv, Options& o) {
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto need = [&](const char* name) -> std::string {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "[ConfigParser] Error: the required argument for option '%s' is missing\n", name);
+        exit(2);
+      }
+      return argv[++i];
+    };
+    auto multi = [&](std::vector<unsigned>& dst) {
+      dst.clear();
+      while (i + 1 < argc && !is_flag(argv[i + 1])) dst.push_back((unsigned)strtoul(argv[++i], nullptr, 10));
+      if (dst.empty()) {
+        fprintf(stderr, "[ConfigParser] Error: option '%s' needs a value\n", a.c_str());
+        exit(2);
+      }
+    };
+    if (a == "-h" || a == "--help") return 1;
+    else if (a == "-s" || a == "--scene-file") o.scene_file = need("scene-file");
+    else if (a == "--scene-type") o.scene_type = need("scene-type");
+    else if (a == "--interactive") o.interactive = parse_bool(need("interactive"));
+    else if (a == "--trials") o.trials = (unsigned)strtoul(need("trials").c_str(), nullptr, 10);
+    else if (a == "-a" || a == "--algorithm") o.algorithm = need("algorithm");
+    else if (a == "-k" || a == "--kernel") o.kernel = need("kernel");
+    else if (a == "--number-of-tiles") multi(o.tiles);
+    else if (a == "--use-unified-memory") o.unified = parse_bool(need("use-unified-memory"));
+    else if (a == "-i" || a == "--iterations") o.iterations = (unsigned)strtoul(need("iterations").c_str(), nullptr, 10);
+    else if (a == "-o" || a == "--output") o.output = need("output");
+    else if (a == "-r" || a == "--resolution") multi(o.resolution);
+    else if (a == "--synthetic") o.synthetic = need("synthetic");
+    else if (a == "--device") o.device = (unsigned)strtoul(need("device").c_str(), nullptr, 10);
+    else if (a == "--seed") o.seed = (unsigned)strtoul(need("seed").c_str(), nullptr, 10);
+    else if (!is_flag(a.c_str()) && o.scene_file.empty()) o.scene_file = a;  // positional
+    else {
+      fprintf(stderr, "[ConfigParser] Error: unrecognised option '%s'\n", a.c_str());
+      return 2;
+    }
+  }
+  if (o.tiles.size() == 1) o.tiles.push_back(o.tiles[0]);
+  if (o.resolution.size() == 1) o.resolution.push_back(o.resolution[0]);
+  return 0;
+}
+
+int scene_type_id(const std::string& t) {
+  if (t == "Auto") return CVR_SCENE_AUTO;
+  if (t == "MitsubaXml") return CVR_SCENE_MITSUBA_XML;
+  if (t == "Vdb") return CVR_SCENE_VDB;
+  if (t == "Raw") return CVR_SCENE_RAW;
+  if (t == "Mhd") return CVR_SCENE_MHD;
+  return -1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Options o;
+  int pr = parse(argc, argv, o);
+  if (pr == 1) {
+    usage();
+    return 0;
+  }
+  if (pr) return pr;
+  if (o.algorithm != "cudaVolPath") {
+    fprintf(stderr, "[ConfigParser] algorithm %s not present in the list of algorithms\n", o.algorithm.c_str());
+    return 2;
+  }
+  const int kernel = cvr_kernel_from_name(o.kernel.c_str());
+  if (kernel == CVR_KERNEL_UNKNOWN) {  // RendererFactory.h:75-76 throws
+    fprintf(stderr, "[RendererFactory] Error: kernel %s unknown\n", o.kernel.c_str());
+    return 2;
+  }
+  cvr_scene* scene = nullptr;
+  int r;
+  if (!o.synthetic.empty()) {
+    r = cvr_scene_synthetic(o.synthetic.c_str(), o.seed, nullptr, &scene);
+  } else {
+    if (o.scene_file.empty()) {
+      fprintf(stderr, "Error: no scene file provided\n");
+      return 2;
+    }
+    const int st = scene_type_id(o.scene_type);
+    if (st < 0) {
+      fprintf(stderr, "Error: scene type not correct\n");
+      return 2;
+    }
+    r = cvr_scene_load(o.scene_file.c_str(), st, &scene);
+  }
+  if (r != CVR_OK) {
+    fprintf(stderr, "Error: could not load scene (%d)\n", r);
+    return 1;
+  }
+  printf("[ConfigParser] kernel set to %s.\n[ConfigParser] iterations set to %u.\n", o.kernel.c_str(), o.iterations);
+  if (o.interactive) printf("[ConfigParser] interactive viewer not available in this build; rendering headless.\n");
+  if (o.output.empty())  // Config::operator<< (Config.h:237-248)
+    o.output = "algorithm_" + o.algorithm + "_kernel_" + o.kernel + "_iter_" + std::to_string(o.iterations);
+
+  cvr_medium_desc md;
+  cvr_scene_medium(scene, &md);
+  const unsigned W = o.resolution[0], H = o.resolution[1];
+  float inv_view[12], r2v[2];
+  cvr_default_camera(W, H, inv_view, r2v);
+  const float full_res[2] = {(float)W, (float)H};
+  std::vector<float> image((size_t)W * H * 4, 0.0f);
+  std::vector<double> times;
+  double mean = 0;
+  for (unsigned t = 0; t < o.trials; ++t) {
+    printf("---------------------------------------------------------------trial : %u \n", t);
+    cvr_ctx* ctx = nullptr;
+    if ((r = cvr_create((int)o.device, kernel, &ctx)) != CVR_OK) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(nullptr));
+      return 1;
+    }
+    cvr_set_seed(ctx, o.seed);
+    if ((r = cvr_set_medium(ctx, &md)) || (r = cvr_set_camera(ctx, inv_view, r2v, full_res)) || (r = cvr_init(ctx))) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
+      return 1;
+    }
+    cvr_render_desc d = {{W, H}, {o.tiles[0], o.tiles[1]}, o.iterations};
+    cvr_stats st;
+    const auto t0 = std::chrono::steady_clock::now();
+    r = cvr_render_image(ctx, &d, nullptr, image.data(), &st);
+    const auto t1 = std::chrono::steady_clock::now();
+    if (r != CVR_OK) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
+      return 1;
+    }
+    const double sec = std::chrono::duration<double>(t1 - t0).count();
+    printf("rendering time      : %.2f sec \n", sec);
+    printf("total traced rays %llu (woodcock steps %llu)\n", (unsigned long long)st.segments,
+           (unsigned long long)st.steps);
+    if (t > 0) {
+      times.push_back(sec);
+      mean += sec;
+    }
+    cvr_destroy(ctx);
+    cvr_write_hdr((o.output + ".hdr").c_str(), image.data(), W, H);
+  }
+  if (o.trials > 1) {
+    mean /= (double)times.size();
+    double var = 0;
+    for (double x : times) var += (x - mean) * (x - mean);
+    var /= (double)times.size();
+    printf("execution mean time of %.2f sec on %zu iterations and std %.5f \n", mean, times.size(), std::sqrt(var));
+    printf("paths per sec %lf \n", (double)W * H * o.iterations / mean);
+  }
+  cvr_scene_destroy(scene);
+  return 0;
+}

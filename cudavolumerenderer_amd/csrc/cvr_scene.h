@@ -1,0 +1,26 @@
+// cvr_scene.h - host-side scene representation behind the opaque cvr_scene.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+struct cvr_scene {
+  std::string name;
+  uint32_t dims[3] = {0, 0, 0};
+  std::vector<float> density;  // x fastest
+  std::vector<float> albedo;   // rgba per voxel
+  float box_min[3] = {-0.5f, -0.5f, -0.5f};
+  float box_max[3] = {0.5f, 0.5f, 0.5f};
+  float scale = 1.0f;
+  float max_density = 1.0f;
+  std::vector<uint8_t> raw;  // raw loader input bytes (for fixtures)
+};
+
+namespace cvr {
+int scene_from_raw_bytes(const std::vector<uint8_t>& raw, const std::string& name, cvr_scene* s);
+void finish_vdb_like(cvr_scene* s);
+int load_vdb_scene(const std::string& path, cvr_scene* s);
+int load_mhd_scene(const std::string& path, cvr_scene* s);
+}  // namespace cvr

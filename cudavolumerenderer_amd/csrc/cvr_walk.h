@@ -1,0 +1,462 @@
+// cvr_walk.h - device building blocks of the volumetric random walk (gfx950).
+//
+// Each function restates one piece of the reference hot path
+// (Fe0437/CudaVolumeRenderer implementation/src, cited per function) with the
+// exact operation order of oracle/cvr_oracle.c, so that one path traced here
+// is bit-identical to the same path traced by the CPU oracle.  Compiled with
+// -ffp-contract=off; the only fused multiply-adds are the explicit det_fmaf
+// calls (Woodcock step, Woodcock position, trilinear lerps, RNG mapping).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "cvr_detmath.h"
+
+namespace cvr {
+
+#define CVR_DEV __device__ __forceinline__
+
+// ------------------------------------------------------------- vectors ----
+struct V3 {
+  float x, y, z;
+};
+CVR_DEV V3 mk3(float x, float y, float z) { return V3{x, y, z}; }
+CVR_DEV V3 add3(V3 a, V3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+CVR_DEV V3 sub3(V3 a, V3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+CVR_DEV V3 mul3(V3 a, V3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+CVR_DEV V3 div3(V3 a, V3 b) { return mk3(a.x / b.x, a.y / b.y, a.z / b.z); }
+CVR_DEV V3 scl3(V3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+CVR_DEV V3 neg3(V3 a) { return mk3(-a.x, -a.y, -a.z); }
+CVR_DEV float dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+CVR_DEV V3 cross3(V3 a, V3 b) {
+  return mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+// helper_math.h:1055 normalize(v) = v*rsqrtf(dot); restated with a correctly
+// rounded 1/sqrtf so host and device agree.
+CVR_DEV V3 normalize3(V3 v) { return scl3(v, 1.0f / det_sqrtf(dot3(v, v))); }
+
+// ----------------------------------------------------------------- RNG ----
+// cuRAND XORWOW, curand_init(seed, 0, 0) + curand_uniform (Rng.h:22-30).
+struct Rng {
+  uint32_t v0, v1, v2, v3, v4, d;
+};
+CVR_DEV void rng_init(Rng& s, int32_t seed) {
+  // Rng(int) -> unsigned long long: sign extension
+  const unsigned long long sd = (unsigned long long)(long long)seed;
+  const uint32_t s0 = ((uint32_t)sd) ^ 0xaad26b49u;
+  const uint32_t s1 = ((uint32_t)(sd >> 32)) ^ 0xf7dcefddu;
+  const uint32_t t0 = 1099087573u * s0;
+  const uint32_t t1 = 2591861531u * s1;
+  s.d = 6615241u + t1 + t0;
+  s.v0 = 123456789u + t0;
+  s.v1 = 362436069u ^ t0;
+  s.v2 = 521288629u + t1;
+  s.v3 = 88675123u ^ t1;
+  s.v4 = 5783321u + t0;
+}
+CVR_DEV uint32_t rng_next(Rng& s) {
+  const uint32_t t = s.v0 ^ (s.v0 >> 2);
+  s.v0 = s.v1;
+  s.v1 = s.v2;
+  s.v2 = s.v3;
+  s.v3 = s.v4;
+  s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+  s.d += 362437u;
+  return s.v4 + s.d;
+}
+CVR_DEV float rng_float(Rng& s) {
+  return det_fmaf((float)rng_next(s), 2.3283064e-10f, 1.1641532e-10f);
+}
+
+// ------------------------------------------------------ kernel params -----
+struct MediumParams {
+  const float* __restrict__ density;  // rx*ry*rz fp32, x fastest
+  const float4* __restrict__ albedo;  // rx*ry*rz float4 (rgb, w=1)
+  uint32_t rx, ry, rz;
+  float gx, gy, gz;  // (float)(res-1): DeviceVolume::volumeToGrid
+  V3 bmin, bmax;
+  V3 shift;          // box_min / extent  (worldToAABB precedence, Q4)
+  float scale;
+  float inv_sigma;   // 1 / (scale * max_density)
+  float g;           // HG asymmetry (0 in the reference, Q7)
+  float ax, ay;      // GGX roughness
+  float eta;         // int_ior / ext_ior
+};
+
+struct LaunchParams {
+  float M[12];            // c_inv_view_mat
+  float r2v[2];           // c_raster_to_view
+  float full_res[2];      // c_pixel_index_range
+  float tile_res[2];      // c_resolution
+  uint32_t off[2];        // c_offset
+  uint32_t tile_px;       // (uint)(c_resolution.x * c_resolution.y)
+  uint32_t tile_w;        // (uint)c_resolution.x
+  uint32_t path_first;    // first path id of this launch
+  uint32_t path_count;    // number of path ids
+  uint32_t seed_base;     // RNG seed = seed_base + path_id
+  uint32_t max_segments;  // safety cap (0 = none)
+  float4* out;            // tile accumulator, tile_px float4
+  unsigned int* queue;    // [0] work-queue head (zeroed per launch)
+  unsigned long long* stats;  // CVR_STAT_* counters (zeroed per launch)
+  uint32_t chunk;         // paths per wave dequeue
+  uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
+};
+
+enum {
+  STAT_PATHS = 0,
+  STAT_SEGMENTS,
+  STAT_STEPS,
+  STAT_DENSITY,
+  STAT_ALBEDO,
+  STAT_ESCAPED,
+  STAT_TRUNCATED,
+  STAT_COUNT
+};
+
+// -------------------------------------------------------- grid lookup -----
+// Volume.h:47-69 + RenderKernelLauncher.cu:20-25: point taps, clamp, the int
+// index goes through uint so -1 clamps to res-1 (Q5).
+CVR_DEV uint32_t texel(int i, uint32_t res) {
+  const uint32_t u = (uint32_t)i;
+  return u < res - 1u ? u : res - 1u;
+}
+CVR_DEV float lerpf(float a, float b, float f, float fi) { return det_fmaf(b, f, a * fi); }
+
+struct Tri {
+  uint32_t xa, xb, ya, yb, za, zb;
+  float fx, fy, fz;
+};
+CVR_DEV Tri tri_setup(const MediumParams& m, V3 p) {
+  const float cx = p.x * m.gx, cy = p.y * m.gy, cz = p.z * m.gz;
+  const int x1 = det_floor_i32(cx), y1 = det_floor_i32(cy), z1 = det_floor_i32(cz);
+  Tri t;
+  t.fx = cx - (float)x1;
+  t.fy = cy - (float)y1;
+  t.fz = cz - (float)z1;
+  t.xa = texel(x1, m.rx);
+  t.xb = texel(x1 + 1, m.rx);
+  t.ya = texel(y1, m.ry);
+  t.yb = texel(y1 + 1, m.ry);
+  t.za = texel(z1, m.rz);
+  t.zb = texel(z1 + 1, m.rz);
+  return t;
+}
+CVR_DEV float density_lookup(const MediumParams& m, V3 p) {
+  const Tri t = tri_setup(m, p);
+  const float* __restrict__ D = m.density;
+  const uint32_t r00 = (t.za * m.ry + t.ya) * m.rx, r01 = (t.za * m.ry + t.yb) * m.rx;
+  const uint32_t r10 = (t.zb * m.ry + t.ya) * m.rx, r11 = (t.zb * m.ry + t.yb) * m.rx;
+  const float d000 = D[r00 + t.xa], d001 = D[r00 + t.xb];
+  const float d010 = D[r01 + t.xa], d011 = D[r01 + t.xb];
+  const float d100 = D[r10 + t.xa], d101 = D[r10 + t.xb];
+  const float d110 = D[r11 + t.xa], d111 = D[r11 + t.xb];
+  const float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
+  const float a = lerpf(lerpf(d000, d001, t.fx, _fx), lerpf(d010, d011, t.fx, _fx), t.fy, _fy);
+  const float b = lerpf(lerpf(d100, d101, t.fx, _fx), lerpf(d110, d111, t.fx, _fx), t.fy, _fy);
+  return lerpf(a, b, t.fz, _fz);
+}
+CVR_DEV V3 albedo_lookup(const MediumParams& m, V3 p) {
+  const Tri t = tri_setup(m, p);
+  const float4* __restrict__ A = m.albedo;
+  const uint32_t r00 = (t.za * m.ry + t.ya) * m.rx, r01 = (t.za * m.ry + t.yb) * m.rx;
+  const uint32_t r10 = (t.zb * m.ry + t.ya) * m.rx, r11 = (t.zb * m.ry + t.yb) * m.rx;
+  const float4 d000 = A[r00 + t.xa], d001 = A[r00 + t.xb];
+  const float4 d010 = A[r01 + t.xa], d011 = A[r01 + t.xb];
+  const float4 d100 = A[r10 + t.xa], d101 = A[r10 + t.xb];
+  const float4 d110 = A[r11 + t.xa], d111 = A[r11 + t.xb];
+  const float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
+#define CVR_TRI(c)                                                                     \
+  lerpf(lerpf(lerpf(d000.c, d001.c, t.fx, _fx), lerpf(d010.c, d011.c, t.fx, _fx), t.fy, \
+              _fy),                                                                    \
+        lerpf(lerpf(d100.c, d101.c, t.fx, _fx), lerpf(d110.c, d111.c, t.fx, _fx), t.fy, \
+              _fy),                                                                    \
+        t.fz, _fz)
+  const V3 r = mk3(CVR_TRI(x), CVR_TRI(y), CVR_TRI(z));
+#undef CVR_TRI
+  return r;
+}
+
+// ---------------------------------------------------------------- AABB ----
+// Geometry.h:55-92.  `normal` persists when no plane matches.
+struct Isect {
+  float dist;
+  V3 normal;
+  bool inside;
+};
+CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
+  const V3 invR = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const V3 tbot = mul3(invR, sub3(m.bmin, o));
+  const V3 ttop = mul3(invR, sub3(m.bmax, o));
+  const V3 tmin = mk3(det_fminf(ttop.x, tbot.x), det_fminf(ttop.y, tbot.y), det_fminf(ttop.z, tbot.z));
+  const V3 tmax = mk3(det_fmaxf(ttop.x, tbot.x), det_fmaxf(ttop.y, tbot.y), det_fmaxf(ttop.z, tbot.z));
+  const float largest_tmin = det_fmaxf(det_fmaxf(tmin.x, tmin.y), det_fmaxf(tmin.x, tmin.z));
+  const float smallest_tmax = det_fminf(det_fminf(tmax.x, tmax.y), det_fminf(tmax.x, tmax.z));
+  is.dist = (largest_tmin > CVR_EPSILON_F) ? largest_tmin : smallest_tmax;
+  if (is.dist == ttop.x) is.normal = mk3(1, 0, 0);
+  else if (is.dist == ttop.y) is.normal = mk3(0, 1, 0);
+  else if (is.dist == ttop.z) is.normal = mk3(0, 0, 1);
+  else if (is.dist == tbot.x) is.normal = mk3(-1, 0, 0);
+  else if (is.dist == tbot.y) is.normal = mk3(0, -1, 0);
+  else if (is.dist == tbot.z) is.normal = mk3(0, 0, -1);
+  is.inside = dot3(is.normal, d) > 0.0f;
+  return (smallest_tmax > largest_tmin) && (is.dist > 0.0f);
+}
+
+// ---------------------------------------------------------- Woodcock ------
+// One Woodcock step (Utilities.cuh:134-136,148-152).  Returns 0 = keep
+// tracking, 1 = tentative t beyond max_t (no collision), 2 = accepted.
+CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
+                          uint32_t& n_steps, uint32_t& n_density) {
+  const float xi = rng_float(rng);
+  t = det_fmaf(-det_logf(det_fmaxf(xi, CVR_EPSILON_F)), m.inv_sigma, t);
+  ++n_steps;
+  if (!(t <= max_t)) return 1;
+  const V3 p = mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z));
+  const float rho = m.scale * density_lookup(m, sub3(p, m.shift));
+  ++n_density;
+  if (!(rho * m.inv_sigma < rng_float(rng))) return 2;
+  return 0;
+}
+
+// --------------------------------------------------------------- HG -------
+// HG.h:11-63
+CVR_DEV V3 hg_sample(V3 v, float g, float e1, float e2) {
+  float cosT;
+  if (det_fabsf(g) > CVR_EPSILON_F) {
+    const float sq = (1.0f - g * g) / ((1.0f - g) + (2.0f * g) * e1);
+    cosT = ((1.0f + g * g) - sq * sq) / (2.0f * det_fabsf(g));
+  } else {
+    cosT = 1.0f - 2.0f * e1;
+  }
+  const float sinT = det_sqrtf(det_fmaxf(0.0f, 1.0f - cosT * cosT));
+  const float phi = CVR_TWOPI_F * e2;
+  const float invN = 1.0f / det_sqrtf(v.x * v.x + v.z * v.z);
+  const V3 v1 = mk3(v.z * invN, 0.0f, (-v.x) * invN);
+  const V3 v2 = cross3(v, v1);
+  float sp, cp;
+  det_sincosf(phi, &sp, &cp);
+  return add3(add3(scl3(v1, sinT * cp), scl3(v2, sinT * sp)), scl3(v, cosT));
+}
+
+// -------------------------------------------------------------- GGX -------
+// GGX.h:13-38
+CVR_DEV float fresnel_dielectric(float eta, float ndotwi, float& ndotwt) {
+  if (eta == 1.0f) {
+    ndotwt = -ndotwi;
+    return 0.0f;
+  }
+  const float scale = (ndotwi > 0.0f) ? 1.0f / eta : eta;
+  const float sin_sqr = 1.0f - ndotwi * ndotwi;
+  const float ndotwt_sqr = 1.0f - (sin_sqr * scale) * scale;
+  if (ndotwt_sqr <= 0.0f) {
+    ndotwt = 0.0f;
+    return 1.0f;
+  }
+  const float a_wi = det_fabsf(ndotwi);
+  const float a_wt = det_sqrtf(ndotwt_sqr);
+  const float Rs = (a_wi - eta * a_wt) / (a_wi + eta * a_wt);
+  const float Rp = (eta * a_wi - a_wt) / (eta * a_wi + a_wt);
+  ndotwt = (ndotwi > 0.0f) ? -a_wt : a_wt;
+  return 0.5f * (Rs * Rs + Rp * Rp);
+}
+// GGX.h:85-144
+CVR_DEV void sample_visible11(float thetaI, float sx, float sy, float& ox, float& oy) {
+  const float phi = (2.0f * CVR_PI_F) * sy;
+  if (thetaI < 1e-4f) {
+    const float r = det_sqrtf(det_fmaxf(0.0f, sx / (1.0f - sx)));
+    float sp, cp;
+    det_sincosf(phi, &sp, &cp);
+    ox = r * cp;
+    oy = r * sp;
+    return;
+  }
+  const float tanThetaI = det_tanf(thetaI);
+  float a = 1.0f / tanThetaI;
+  a = 1.0f + (1.0f / (a * a));
+  const float G1 = 2.0f / (1.0f + det_sqrtf(a));
+  float A = ((2.0f * sx) / G1) - 1.0f;
+  if (det_fabsf(A) == 1.0f) A -= (A < 0.0f ? -1.0f : 1.0f) * CVR_EPSILON_F;
+  const float tmp = 1.0f / (A * A - 1.0f);
+  const float B = tanThetaI;
+  const float D = det_sqrtf(det_fmaxf(0.0f, ((B * B) * tmp) * tmp - (A * A - B * B) * tmp));
+  const float s1 = B * tmp - D, s2 = B * tmp + D;
+  const float slope_x = (A < 0.0f || s2 > 1.0f / tanThetaI) ? s1 : s2;
+  float S;
+  if (sy > 0.5f) {
+    S = 1.0f;
+    sy = 2.0f * (sy - 0.5f);
+  } else {
+    S = -1.0f;
+    sy = 2.0f * (0.5f - sy);
+  }
+  const float z =
+      (sy * (sy * (sy * (-0.365728915865723f) + 0.790235037209296f) - 0.424965825137544f) +
+       0.000152998850436920f) /
+      (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) +
+             1.0f) -
+       0.539825872510702f);
+  ox = slope_x;
+  oy = (S * z) * det_sqrtf(1.0f + slope_x * slope_x);
+}
+// GGX.h:146-181
+CVR_DEV V3 ggx_sample_vndf(V3 wi_, float ax, float ay, float sx, float sy) {
+  const V3 wi = normalize3(mk3(ax * wi_.x, ay * wi_.y, wi_.z));
+  float theta = 0.0f, phi = 0.0f;
+  if (wi.z < 0.999999f) {
+    theta = det_acosf(wi.z);
+    phi = det_atan2f(wi.y, wi.x);
+  }
+  float sinPhi, cosPhi;
+  det_sincosf(phi, &sinPhi, &cosPhi);
+  float slx, sly;
+  sample_visible11(theta, sx, sy, slx, sly);
+  float rx = cosPhi * slx - sinPhi * sly;
+  float ry = sinPhi * slx + cosPhi * sly;
+  rx *= ax;
+  ry *= ay;
+  const float n = 1.0f / det_sqrtf(rx * rx + ry * ry + 1.0f);
+  return mk3(-rx * n, -ry * n, n);
+}
+// GGX.h:213-255
+CVR_DEV float project_roughness(V3 v, float ax, float ay) {
+  const float invSinTheta2 = 1.0f / (1.0f - v.z * v.z);
+  if (ax == ay || invSinTheta2 <= 0.0f) return ax;
+  const float cosPhi2 = v.x * v.x * invSinTheta2;
+  const float sinPhi2 = v.y * v.y * invSinTheta2;
+  return det_sqrtf(cosPhi2 * ax * ax + sinPhi2 * ay * ay);
+}
+CVR_DEV float ggx_g1(float ax, float ay, V3 v, V3 m) {
+  if (dot3(v, m) * v.z <= 0.0f) return 0.0f;
+  const float temp = 1.0f - v.z * v.z;
+  if (temp <= 0.0f) return 0.0f;
+  const float tn = det_fabsf(det_sqrtf(temp) / v.z);
+  if (tn == 0.0f) return 1.0f;
+  const float root = project_roughness(v, ax, ay) * tn;
+  return 2.0f / (1.0f + det_sqrtf(1.0f + root * root));
+}
+// GGX.h:265-326; `wo` aliases the path direction (Q8).
+CVR_DEV bool ggx_sample(const MediumParams& m, V3 wi, Rng& rng, V3& wo, float& weight) {
+  const float ndotwi = wi.z;
+  if (ndotwi == 0.0f) {
+    weight = 0.0f;
+    return false;
+  }
+  weight = 1.0f;
+  const float sign = wi.z / det_fabsf(wi.z);
+  const float s0 = rng_float(rng);
+  const float s1 = rng_float(rng);
+  const V3 wh = ggx_sample_vndf(scl3(wi, sign), m.ax, m.ay, s0, s1);
+  float whdotwt = __builtin_nanf("");
+  const float whdotwi = dot3(wh, wi);
+  const float F = fresnel_dielectric(m.eta, whdotwi, whdotwt);
+  if (rng_float(rng) <= F) {
+    wo = sub3(scl3(wh, 2.0f * whdotwi), wi);
+    if (wi.z * wo.z <= 0.0f) {
+      weight = 0.0f;
+      return false;
+    }
+  } else {
+    if (whdotwt == 0.0f) {
+      weight = 0.0f;
+      return false;
+    }
+    float eta = m.eta;
+    if (whdotwt < 0.0f) eta = 1.0f / eta;
+    wo = sub3(scl3(wh, whdotwi * eta + whdotwt), scl3(wi, eta));
+    if (wi.z * wo.z >= 0.0f) {
+      weight = 0.0f;
+      return false;
+    }
+  }
+  weight *= ggx_g1(m.ax, m.ay, wo, wh);
+  return true;
+}
+
+// ------------------------------------------------------------- frame ------
+// CVRMath.h:58-91
+struct Frame {
+  V3 x, y, z;
+};
+CVR_DEV Frame frame_from_z(V3 n) {
+  Frame f;
+  f.z = normalize3(n);
+  const V3 tx = (det_fabsf(f.z.x) > 0.99f) ? mk3(0, 1, 0) : mk3(1, 0, 0);
+  f.y = normalize3(cross3(f.z, tx));
+  f.x = cross3(f.y, f.z);
+  return f;
+}
+CVR_DEV V3 frame_to_local(const Frame& f, V3 a) { return mk3(dot3(a, f.x), dot3(a, f.y), dot3(a, f.z)); }
+CVR_DEV V3 frame_to_world(const Frame& f, V3 a) {
+  return add3(add3(scl3(f.x, a.x), scl3(f.y, a.y)), scl3(f.z, a.z));
+}
+
+// ------------------------------------------------------------ camera ------
+// NaiveVolPTsk_kernel.cuh:22-31 / RegenerationVolPTsk_kernel.cuh:169-177 and
+// Utilities.cuh:180-213: path_id -> (image_id, seeded RNG, camera ray).
+struct PathState {
+  Rng rng;
+  V3 o, d, T;
+  uint32_t image_id;
+};
+CVR_DEV void path_begin(const LaunchParams& L, uint32_t path_id, PathState& ps) {
+  ps.image_id = path_id % L.tile_px;
+  rng_init(ps.rng, (int32_t)(L.seed_base + path_id));
+  const float px = (float)(ps.image_id % L.tile_w) + (float)L.off[0];
+  const float py = det_floorf((float)ps.image_id / L.tile_res[0]) + (float)L.off[1];
+  const float r0 = rng_float(ps.rng);
+  const float r1 = rng_float(ps.rng);
+  float rx = ((px + r0) * 2.0f) / L.full_res[0] - 1.0f;
+  float ry = ((py + r1) * 2.0f) / L.full_res[1] - 1.0f;
+  rx = L.r2v[0] * rx;
+  ry = L.r2v[1] * ry;
+  const float* M = L.M;
+  ps.o = mk3(0.0f * M[0] + 0.0f * M[1] + 0.0f * M[2] + 1.0f * M[3],
+             0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7],
+             0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11]);
+  const V3 v = normalize3(mk3(rx, ry, 1.0f));
+  ps.d = mk3(dot3(v, mk3(M[0], M[1], M[2])), dot3(v, mk3(M[4], M[5], M[6])),
+             dot3(v, mk3(M[8], M[9], M[10])));
+  ps.T = mk3(1.0f, 1.0f, 1.0f);
+}
+
+// Boundary event (NaiveVolPTsk_kernel.cuh:53-65): GGX at the AABB surface.
+CVR_DEV void boundary_event(const MediumParams& m, PathState& ps, const Isect& is) {
+  const Frame fr = frame_from_z(is.normal);
+  const V3 dir = frame_to_local(fr, normalize3(neg3(ps.d)));
+  ps.o = add3(ps.o, scl3(ps.d, is.dist));
+  float weight = 1.0f;
+  if (ggx_sample(m, dir, ps.rng, ps.d, weight)) {
+    ps.T = scl3(ps.T, weight);
+    ps.d = frame_to_world(fr, ps.d);
+    ps.o = add3(ps.o, scl3(ps.d, CVR_EPSILON_F));
+  }
+}
+// Real collision (NaiveVolPTsk_kernel.cuh:66-72; regeneration :212 has no -eps).
+template <bool kScatterEps>
+CVR_DEV void scatter_event(const MediumParams& m, PathState& ps, float t) {
+  ps.o = add3(ps.o, scl3(ps.d, t));
+  if (kScatterEps) ps.o = sub3(ps.o, scl3(ps.d, CVR_EPSILON_F));
+  const V3 a = albedo_lookup(m, div3(sub3(ps.o, m.bmin), sub3(m.bmax, m.bmin)));
+  ps.T = mul3(ps.T, a);
+  const float e1 = rng_float(ps.rng);
+  const float e2 = rng_float(ps.rng);
+  ps.d = hg_sample(ps.d, m.g, e1, e2);
+}
+// Russian roulette (NaiveVolPTsk_kernel.cuh:75-84).  Returns false = path dies.
+CVR_DEV bool roulette(PathState& ps) {
+  const float p = det_fminf(1.0f, det_fmaxf(det_fmaxf(ps.T.x, ps.T.y), ps.T.z));
+  if (rng_float(ps.rng) > p) return false;
+  ps.T = mk3(ps.T.x / p, ps.T.y / p, ps.T.z / p);
+  return true;
+}
+// atomicVectorAdd (Utilities.cuh:15-22) with Le = 1.
+CVR_DEV void splat(const LaunchParams& L, const PathState& ps) {
+  float* px = reinterpret_cast<float*>(L.out + ps.image_id);
+  atomicAdd(px + 0, ps.T.x);
+  atomicAdd(px + 1, ps.T.y);
+  atomicAdd(px + 2, ps.T.z);
+  px[3] = 1.0f;
+}
+
+}  // namespace cvr

@@ -1,0 +1,42 @@
+"""Multi-GPU driver: one process per GPU, sample (path-id) sharding, one
+RCCL all-reduce of the framebuffer.
+
+Why this decomposition: paths are independent and the only
+shared output is the additive fp32 framebuffer.  With the RNG bound to the
+path id, a path renders the same on any rank, so splitting the path-id range
+[0, n_paths) into contiguous shards changes nothing but the order of the fp32
+sums.  The only exchange is one sum-reduce of W*H*4 floats over xGMI (16 MiB
+at 1024^2) per render.  Image tiles are not used for the split because tile
+costs are very uneven (background vs volume).
+
+Weak scaling (bench.py): each rank renders its own `iterations` samples per
+pixel; the job renders iterations*world samples per pixel in total.
+"""
+from __future__ import annotations
+
+from typing import Callable, Tuple
+
+
+def shard_range(n_paths: int, rank: int, world: int) -> Tuple[int, int]:
+    """Contiguous path-id shard [first, first+count) of rank `rank`."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    base, rem = divmod(n_paths, world)
+    first = rank * base + min(rank, rem)
+    count = base + (1 if rank < rem else 0)
+    return first, count
+
+
+def render_sharded(render_range: Callable[[int, int], "object"], n_paths: int, rank: int, world: int,
+                   all_reduce: Callable[["object"], None] | None):
+    """Render this rank's shard into an accumulator, then sum over ranks.
+
+    `render_range(first, count)` returns the rank's unnormalised accumulator
+    (a torch tensor on the rank's device, or any tensor the reducer accepts);
+    `all_reduce(acc)` sums it in place across ranks (torch.distributed
+    all_reduce over RCCL on the GPU box, gloo in the CPU tests)."""
+    first, count = shard_range(n_paths, rank, world)
+    acc = render_range(first, count)
+    if world > 1 and all_reduce is not None:
+        all_reduce(acc)
+    return acc

@@ -1,0 +1,207 @@
+/*
+ * cvr.h - C ABI of the MI355X volumetric path tracer (libcvr.so).
+ *
+ * This is the drop-in boundary for the reference's kernel-launcher layer
+ * (Fe0437/CudaVolumeRenderer, implementation/src/RenderKernelLauncher.h:20-174)
+ * and for the CudaVolPath driver above it (CudaVolPath.{h,cpp}).  Plain C
+ * types only: pointers, sizes, status codes.  Every call returns 0 (CVR_OK) or
+ * a negative CVR_ERR_* and never exits the process (the reference's
+ * CHECK_CUDA_ERROR calls exit(), Debug.h:19-37); the message is available from
+ * cvr_last_error().
+ *
+ * Unlike the reference, launch parameters live in a per-context struct passed
+ * by value to the kernels (the reference keeps them in module-global
+ * __constant__ symbols, RenderKernelLauncher.cu:67-72), so one process can
+ * hold one context per GPU.
+ */
+#ifndef CVR_H_
+#define CVR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CVR_ABI_VERSION 1
+
+enum {
+  CVR_OK = 0,
+  CVR_ERR_INVALID = -1,     /* bad argument */
+  CVR_ERR_HIP = -2,         /* HIP runtime failure */
+  CVR_ERR_STATE = -3,       /* call out of lifecycle order */
+  CVR_ERR_IO = -4,          /* file / parse error */
+  CVR_ERR_UNSUPPORTED = -5, /* kernel or feature not available */
+  CVR_ERR_NOMEM = -6
+};
+
+/* Config::Kernel order and names (Config.h:87-95, :210-213). */
+typedef enum {
+  CVR_KERNEL_NAIVE_SK = 0,
+  CVR_KERNEL_NAIVE_MK = 1,
+  CVR_KERNEL_REGENERATION_SK = 2,
+  CVR_KERNEL_STREAMING_MK = 3,
+  CVR_KERNEL_STREAMING_SK = 4,
+  CVR_KERNEL_SORTING_SK = 5,
+  CVR_KERNEL_UNKNOWN = 6
+} cvr_kernel;
+
+/* Scene type names of the --scene-type flag (ConfigParser.cpp:16-18). */
+typedef enum {
+  CVR_SCENE_AUTO = 0,
+  CVR_SCENE_MITSUBA_XML = 1,
+  CVR_SCENE_VDB = 2,
+  CVR_SCENE_RAW = 3,
+  CVR_SCENE_MHD = 4
+} cvr_scene_type;
+
+/* Options for cvr_set_option. */
+typedef enum {
+  CVR_OPT_MAX_SEGMENTS = 1,   /* safety cap on segments per path (default 1<<20, 0 = none) */
+  CVR_OPT_CHUNK = 2,          /* paths per wave dequeue (persistent schedulers) */
+  CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
+  CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
+  CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
+  CVR_OPT_SCHEDULER = 6,      /* persistent kernels: 0 wavefront (default), 1 single kernel */
+  CVR_OPT_POOL = 7,           /* wavefront ray-slot pool size (default 2^21) */
+  CVR_OPT_TIMING = 8          /* 1: time every wavefront kernel (track_ms / events_ms) */
+} cvr_option;
+
+/* HeterogeneousMedium + GGX boundary (Medium.h:110-190, Bsdf.h:17-30). */
+typedef struct cvr_medium_desc {
+  uint32_t res[3];        /* grid resolution x, y, z */
+  const float* density;   /* host, res[0]*res[1]*res[2] fp32, x fastest */
+  const float* albedo;    /* host, same grid, 4 floats per voxel (r,g,b,1) */
+  float box_min[3];       /* AABB (density_AABB) */
+  float box_max[3];
+  float scale;            /* density scale (VDB 100, Raw 40) */
+  float max_density;      /* majorant / scale */
+  float g;                /* HG asymmetry; the reference never uploads it (Q7): 0 */
+  float roughness[2];     /* GGX alpha (0.1, 0.1) */
+  float eta;              /* int_ior / ext_ior (1.05f / 1.01f) */
+} cvr_medium_desc;
+
+typedef struct cvr_stats {
+  uint64_t paths;      /* paths started */
+  uint64_t segments;   /* loop iterations (RAYS_STATISTICS count) */
+  uint64_t steps;      /* Woodcock steps drawn */
+  uint64_t density;    /* density evaluations (8 fp32 taps each) */
+  uint64_t albedo;     /* albedo evaluations (8 float4 taps each) */
+  uint64_t escaped;    /* paths that splatted into the framebuffer */
+  uint64_t truncated;  /* paths cut by CVR_OPT_MAX_SEGMENTS */
+  double kernel_ms;    /* device time of the last launch (HIP events) */
+  uint64_t iterations; /* wavefront: events/track kernel pairs of the last launch */
+  double track_ms;     /* wavefront: summed device time of the tracking kernels (CVR_OPT_TIMING) */
+  double events_ms;    /* wavefront: summed device time of the event kernels (CVR_OPT_TIMING) */
+} cvr_stats;
+
+typedef struct cvr_path_record {
+  uint32_t image_id;
+  uint32_t flags; /* bit0 escaped, bit1 truncated */
+  float T[3];
+  uint32_t n_segments, n_steps, n_density, n_albedo;
+} cvr_path_record;
+
+typedef struct cvr_ctx cvr_ctx;
+typedef struct cvr_scene cvr_scene;
+
+/* ---- lifecycle (RenderKernelLauncher.h:20-52) ------------------------- */
+int cvr_create(int device, int kernel, cvr_ctx** out);
+int cvr_destroy(cvr_ctx* ctx);
+const char* cvr_last_error(const cvr_ctx* ctx); /* ctx may be NULL */
+int cvr_abi_version(void);
+
+/* setScene + createTextureWithVolume (CudaVolPath.cpp:88-186): copies the
+ * host volumes into HBM (the caller keeps ownership of the host arrays). */
+int cvr_set_medium(cvr_ctx* ctx, const cvr_medium_desc* medium);
+/* copyInvViewMatrix (12 floats), copyRasterToView, copyPixelIndexRange */
+int cvr_set_camera(cvr_ctx* ctx, const float inv_view[12], const float raster_to_view[2],
+                   const float full_res[2]);
+/* setResolution(tile_dim) */
+int cvr_set_resolution(cvr_ctx* ctx, uint32_t tile_w, uint32_t tile_h);
+/* copyOffset(tile origin) */
+int cvr_set_offset(cvr_ctx* ctx, uint32_t x, uint32_t y);
+/* setNIterations: n_paths = tile_w * tile_h * iterations */
+int cvr_set_iterations(cvr_ctx* ctx, uint32_t iterations);
+/* Extension for sharding: launch only path ids [first, first+count) of the
+ * tile's n_paths (default: all). */
+int cvr_set_path_range(cvr_ctx* ctx, uint64_t first, uint64_t count);
+/* RNG seed base (RegenerationVolPTsk_kernel.cuh:18 `seed`); path p uses
+ * curand_init(seed + p). */
+int cvr_set_seed(cvr_ctx* ctx, uint32_t seed);
+int cvr_get_seed(const cvr_ctx* ctx, uint32_t* seed);
+/* setOutputPtr: device float4 tile buffer; NULL selects a context-owned one. */
+int cvr_set_output(cvr_ctx* ctx, void* device_tile_buffer);
+void* cvr_output_ptr(cvr_ctx* ctx);
+/* Run on a caller stream (hipStream_t), e.g. a framework's current stream;
+ * NULL is the device's null stream.  cvr_own_stream() returns the
+ * non-blocking stream the context creates for itself (the default). */
+int cvr_set_stream(cvr_ctx* ctx, void* hip_stream);
+void* cvr_own_stream(cvr_ctx* ctx);
+int cvr_set_option(cvr_ctx* ctx, int option, int64_t value);
+/* init(): occupancy-based launch sizing (Occupancy.cuh:24-70). */
+int cvr_init(cvr_ctx* ctx);
+/* launchRender(): asynchronous on the context stream; accumulates into the
+ * output buffer. */
+int cvr_launch_render(cvr_ctx* ctx);
+/* reset(): synchronise, rewind the work queue, advance the seed by n_paths
+ * for regenerationSK (RenderKernelLauncher.cu:353-361). */
+int cvr_reset(cvr_ctx* ctx);
+int cvr_synchronize(cvr_ctx* ctx);
+/* memset of the tile buffer (CudaVolPath.cpp:194-209). */
+int cvr_clear_output(cvr_ctx* ctx);
+/* Counters of the last launch (RAYS_STATISTICS analogue) + its device time. */
+int cvr_get_stats(cvr_ctx* ctx, cvr_stats* stats);
+/* D->H copy of the tile buffer, every component divided by `scale`. */
+int cvr_copy_output(cvr_ctx* ctx, float* host_rgba, float scale);
+/* Debug/parity: trace path ids [first, first+count) one per work-item and
+ * return per-path records (no framebuffer splat). */
+int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_record* host_out);
+/* Device properties used for sizing: CU count, persistent grid. */
+int cvr_device_info(cvr_ctx* ctx, int* cu_count, int* persistent_grid);
+
+/* ---- renderer (CudaVolPath::render, CudaVolPath.cpp:339-347) ---------- */
+typedef struct cvr_render_desc {
+  uint32_t resolution[2]; /* full image W, H */
+  uint32_t n_tiles[2];    /* --number-of-tiles (TilingConfig, Config.h:61-78) */
+  uint32_t iterations;    /* --iterations */
+} cvr_render_desc;
+/* Render all tiles: per tile set offset, launch, normalise by iterations
+ * into the image, reset.  `device_image` (W*H float4, may be NULL) receives
+ * the normalised image on the device, `host_image` (may be NULL) a copy.
+ * Pixels outside tile_dim*n_tiles are not written (Q1). */
+int cvr_render_image(cvr_ctx* ctx, const cvr_render_desc* desc, void* device_image, float* host_image,
+                     cvr_stats* stats);
+
+/* ---- camera / tiling helpers ------------------------------------------ */
+/* Default Camera (Camera.h:25-71, MITSUBA_COMPARABLE) after
+ * setResolution(w,h), flattened as CudaVolPath::initCamera (CudaVolPath.cpp:67-85). */
+int cvr_default_camera(uint32_t width, uint32_t height, float inv_view[12], float raster_to_view[2]);
+/* TilingConfig (Config.h:61-78) + initTileArray (CudaVolPath.cpp:13-29). */
+int cvr_tiling(uint32_t width, uint32_t height, uint32_t ntx, uint32_t nty, uint32_t tile_dim[2]);
+int cvr_tile_origin(uint32_t tile_id, uint32_t ntx, const uint32_t tile_dim[2], uint32_t origin[2]);
+
+/* ---- scenes (SceneBuilder family, Scene.h:56-81) ----------------------- */
+/* Load a scene file: Raw (RawSceneBuilder.h), Vdb (VDBSceneBuilder.h), Mhd
+ * (convert-mhd semantics), MitsubaXml.  AUTO picks by extension
+ * (ConfigParser.cpp:79-97). */
+int cvr_scene_load(const char* path, int scene_type, cvr_scene** out);
+/* Synthetic proxies for the missing data blobs:
+ * "bucky" (32^3 raw), "manix" (256x230x256 VDB-like), "hetvol" (128x128x50).
+ * dims may be NULL (default size). */
+int cvr_scene_synthetic(const char* name, uint32_t seed, const uint32_t* dims, cvr_scene** out);
+/* Medium description; pointers stay owned by the scene. */
+int cvr_scene_medium(const cvr_scene* scene, cvr_medium_desc* out);
+int cvr_scene_raw_bytes(const cvr_scene* scene, const uint8_t** bytes, size_t* n);
+void cvr_scene_destroy(cvr_scene* scene);
+/* Radiance RGBE .hdr of an RGBA float image (Image::saveHDR, Image.cpp:58-62). */
+int cvr_write_hdr(const char* path, const float* rgba, uint32_t width, uint32_t height);
+/* Kernel name <-> id (Config.h:210-213); unknown -> CVR_KERNEL_UNKNOWN. */
+int cvr_kernel_from_name(const char* name);
+const char* cvr_kernel_name(int kernel);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CVR_H_ */

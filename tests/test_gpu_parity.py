@@ -1,0 +1,214 @@
+"""HIP path vs CPU oracle parity (run on the MI355X box: pytest -m gpu).
+
+Contract:
+  * per path: bit-exact (image_id, flags, T bits, segment/step/tap counts);
+  * per pixel: the only difference is the order of fp32 atomic additions, so
+    |gpu - cpu| <= 2 (n - 1) 2^-24 max(gpu, cpu) for a pixel that receives
+    n <= iterations contributions (plus 1e-30 for zeros);
+  * counters (segments, Woodcock steps, density/albedo taps, escapes): equal.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+NTHREADS = min(16, os.cpu_count() or 1)
+
+
+def make_ctx(cvr, scene, W, H, kernel, seed=0):
+    ctx = cvr.Context(0, kernel)
+    ctx.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(W, H)
+    ctx.set_camera(iv, r2v, (W, H))
+    ctx.set_seed(seed)
+    ctx.init()
+    return ctx, iv, r2v
+
+
+def oracle_for(oracle_mod, scene):
+    return oracle_mod.Oracle.from_medium_desc(scene.medium, scene.density, scene.albedo)
+
+
+def oracle_image(oracle_mod, orc, iv, r2v, W, H, tiles, iters, kernel, seed=0):
+    """The reference's tile loop restated with the oracle (CudaVolPath.cpp:249-347)."""
+    tw, th = W // tiles[0], H // tiles[1]
+    n_paths = tw * th * iters
+    img = np.zeros((H, W, 4), np.float32)
+    stats = {}
+    for k in range(tiles[0] * tiles[1]):
+        ox, oy = tw * (k % tiles[0]), th * int(np.float32(k) / np.float32(tiles[0]))
+        sb = (seed + k * n_paths) & 0xFFFFFFFF if kernel == 2 else seed
+        L = orc.launch(iv, r2v, (W, H), (tw, th), (ox, oy), kernel, sb)
+        tile, st = orc.render(L, 0, n_paths, nthreads=NTHREADS)
+        img[oy:oy + th, ox:ox + tw] = tile / np.float32(iters)
+        for key, v in st.as_dict().items():
+            stats[key] = stats.get(key, 0) + v
+    return img, stats
+
+
+def assert_pixels_close(gpu, cpu, iters):
+    # NaN pixels are reference behaviour: they must
+    # coincide exactly; every other pixel obeys the summation-order bound.
+    ng, nc = np.isnan(gpu), np.isnan(cpu)
+    assert (ng == nc).all(), f"NaN pattern differs: gpu {ng.sum()} cpu {nc.sum()}"
+    gpu = np.where(ng, 0, gpu)
+    cpu = np.where(nc, 0, cpu)
+    bound = 2.0 * max(iters - 1, 1) * 2.0 ** -24 * np.maximum(np.abs(gpu), np.abs(cpu)) + 1e-30
+    diff = np.abs(gpu.astype(np.float64) - cpu.astype(np.float64))
+    bad = diff > bound
+    assert not bad.any(), (f"{bad.sum()} pixels out of tolerance; worst diff {diff.max()} "
+                           f"at {np.unravel_index(np.argmax(diff - bound), diff.shape)}")
+
+
+SCENES = {
+    "bucky": dict(name="bucky"),
+    "manix_small": dict(name="manix", dims=(64, 58, 64)),
+    "hetvol": dict(name="hetvol"),
+}
+
+
+@pytest.fixture(scope="module")
+def scenes(cvr):
+    return {k: cvr.Scene.synthetic(v["name"], 0, v.get("dims")) for k, v in SCENES.items()}
+
+
+@pytest.mark.parametrize("scene_key", list(SCENES))
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel):
+    scene = scenes[scene_key]
+    W = H = 64
+    iters = 3
+    ctx, iv, r2v = make_ctx(cvr, scene, W, H, kernel, seed=7)
+    ctx.set_resolution(W, H)
+    ctx.set_iterations(iters)
+    n = W * H * iters
+    g = ctx.trace_paths(0, n)
+    orc = oracle_for(oracle_mod, scene)
+    kid = cvr.KERNELS.index(kernel)
+    c = orc.trace_paths(orc.launch(iv, r2v, (W, H), (W, H), (0, 0), kid, 7), 0, n)
+    for f in ("image_id", "flags", "n_segments", "n_steps", "n_density", "n_albedo"):
+        mism = np.nonzero(g[f] != c[f])[0]
+        assert mism.size == 0, f"{f} differs for {mism.size} paths, first path {mism[:5]}"
+    tb, cb = g["T"].view(np.uint32), c["T"].view(np.uint32)
+    mism = np.nonzero((tb != cb).any(axis=1))[0]
+    assert mism.size == 0, f"T bits differ for {mism.size} paths, first {mism[:5]}"
+    assert c["n_density"].sum() > 0 and (c["flags"] & 1).any()
+
+
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+@pytest.mark.parametrize("tiles", [(1, 1), (4, 2), (3, 3)])
+def test_render_image_matches_oracle(cvr, oracle_mod, scenes, kernel, tiles):
+    scene = scenes["bucky"]
+    W, H, iters = 96, 96, 4  # 96/3 = 32, 96/4 = 24, 96/2 = 48
+    ctx, iv, r2v = make_ctx(cvr, scene, W, H, kernel)
+    img, st = ctx.render_image(W, H, tiles, iters)
+    ref, rst = oracle_image(oracle_mod, oracle_for(oracle_mod, scene), iv, r2v, W, H, tiles, iters,
+                            cvr.KERNELS.index(kernel))
+    assert_pixels_close(img, ref, iters)
+    for k in ("paths", "segments", "steps", "density", "albedo", "escaped", "truncated"):
+        assert getattr(st, k) == rst[k], k
+
+
+def test_c1_bucky_256_4it(cvr, oracle_mod, scenes):
+    """BASELINE config C1 (bucky 32^3, 256x256, 4 iterations) through naiveSK."""
+    scene = scenes["bucky"]
+    ctx, iv, r2v = make_ctx(cvr, scene, 256, 256, "naiveSK")
+    img, st = ctx.render_image(256, 256, (1, 1), 4)
+    ref, rst = oracle_image(oracle_mod, oracle_for(oracle_mod, scene), iv, r2v, 256, 256, (1, 1), 4, 0)
+    assert_pixels_close(img, ref, 4)
+    assert st.paths == 256 * 256 * 4 and st.steps == rst["steps"]
+
+
+def test_scheduler_knobs_do_not_change_results(cvr, scenes):
+    scene = scenes["manix_small"]
+    W = H = 128
+    base = None
+    # (chunk, event/refill threshold, grid, scheduler, pool): the single
+    # persistent kernel and the wavefront scheduler with pools from 256 slots
+    # (hundreds of events/track iterations) up must all give the same result.
+    for chunk, thresh, grid, sched, pool in [(128, 16, 0, 0, 1 << 21), (64, 1, 0, 0, 256), (256, 64, 0, 0, 4096),
+                                             (32, 8, 7, 0, 1000), (128, 16, 0, 1, 1 << 21), (64, 1, 0, 1, 1 << 21),
+                                             (256, 64, 0, 1, 1 << 21), (32, 8, 7, 1, 1 << 21)]:
+        ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+        ctx.set_option(cvr.OPT_CHUNK, chunk)
+        ctx.set_option(cvr.OPT_EVENT_THRESHOLD, thresh)
+        ctx.set_option(cvr.OPT_GRID, grid)
+        ctx.set_option(cvr.OPT_SCHEDULER, sched)
+        ctx.set_option(cvr.OPT_POOL, pool)
+        img, st = ctx.render_image(W, H, (1, 1), 4)
+        key = (st.paths, st.segments, st.steps, st.density, st.albedo, st.escaped)
+        if base is None:
+            base = (img, key)
+        else:
+            assert key == base[1]
+            assert_pixels_close(img, base[0], 4)
+
+
+def test_naive_without_eps_equals_regeneration(cvr, scenes):
+    """The two schedulers differ only by the scatter -eps."""
+    scene = scenes["hetvol"]
+    W = H = 96
+    a, _, _ = make_ctx(cvr, scene, W, H, "naiveSK")
+    a.set_option(cvr.OPT_SCATTER_EPS, 0)
+    b, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+    ia, sa = a.render_image(W, H, (1, 1), 2)
+    ib, sb = b.render_image(W, H, (1, 1), 2)
+    assert (sa.steps, sa.escaped) == (sb.steps, sb.escaped)
+    assert_pixels_close(ia, ib, 2)
+
+
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+def test_path_range_shards_sum_to_whole(cvr, scenes, kernel):
+    scene = scenes["manix_small"]
+    W = H = 128
+    iters = 4
+    n = W * H * iters
+    whole, _, _ = make_ctx(cvr, scene, W, H, kernel)
+    whole.set_resolution(W, H)
+    whole.set_iterations(iters)
+    whole.clear_output()
+    whole.launch_render()
+    sw = whole.stats()
+    full = whole.copy_output(W, H)
+    parts = np.zeros_like(full)
+    tot = 0
+    bounds = [0, n // 3, n // 2 + 17, n]
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        ctx, _, _ = make_ctx(cvr, scene, W, H, kernel)
+        ctx.set_resolution(W, H)
+        ctx.set_iterations(iters)
+        ctx.set_path_range(a, b - a)
+        ctx.clear_output()
+        ctx.launch_render()
+        tot += ctx.stats().steps
+        parts[..., :3] += ctx.copy_output(W, H)[..., :3]
+    assert tot == sw.steps
+    assert_pixels_close(parts[..., :3], full[..., :3], 3 * iters)
+
+
+def test_c2_manix_1024_full_size_vs_oracle(cvr, oracle_mod):
+    """BASELINE config C2 at full size: manix proxy 256x230x256, 1024^2, 20 it,
+    regenerationSK.  The oracle renders the same 20.97 M paths on the host."""
+    scene = cvr.Scene.synthetic("manix")
+    W = H = 1024
+    ctx, iv, r2v = make_ctx(cvr, scene, W, H, "regenerationSK")
+    img, st = ctx.render_image(W, H, (1, 1), 20)
+    assert st.paths == W * H * 20 and st.truncated == 0
+    ref, rst = oracle_image(oracle_mod, oracle_for(oracle_mod, scene), iv, r2v, W, H, (1, 1), 20, 2)
+    for k in ("segments", "steps", "density", "albedo", "escaped"):
+        assert getattr(st, k) == rst[k], k
+    assert_pixels_close(img, ref, 20)
+
+
+def test_errors_are_reported_not_fatal(cvr, scenes):
+    with pytest.raises(cvr.CvrError) as e:
+        cvr.Context(0, "naiveMK")
+    assert "not implemented" in str(e.value)
+    ctx = cvr.Context(0, "regenerationSK")
+    with pytest.raises(cvr.CvrError) as e:
+        ctx.launch_render()
+    assert "CVR_ERR_STATE" in str(e.value)
+    with pytest.raises(cvr.CvrError):
+        ctx.set_option(cvr.OPT_EVENT_THRESHOLD, 0)

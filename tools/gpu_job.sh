@@ -1,0 +1,37 @@
+#!/bin/bash
+# Runs GPU steps on the gpurun box, each under its own timeout; stops after a
+# timeout / abort / crash (rc >= 124).  Usage: tools/gpu_job.sh step [step...]
+#   steps: info smoke pytest bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {
+  local name=$1 secs=$2; shift 2
+  echo "=== $name (limit ${secs}s): $*"
+  local t0=$(date +%s)
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)"
+  tail -n 25 "$OUT/$name.log"
+  if [ $rc -ge 124 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    info) run info 60 bash -c 'nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -m1 -w fma /proc/cpuinfo; rocm-smi --showproductname 2>/dev/null | head -20; python3 -c "import torch;print(torch.__version__, torch.cuda.device_count())"' ;;
+    smoke) run smoke 400 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q -x --timeout 900 -p no:cacheprovider ;;
+    pytestall) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q --timeout 900 -p no:cacheprovider ;;
+    bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
+    prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmclist) run pmclist 120 rocprofv3 -L ;;
+    tune) run tune 600 python3 tools/tune.py ;;
+    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc_sq" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 1 --variants "regenerationSK:ev=16,chunk=128" ;;
+    *) echo "unknown step $step" ;;
+  esac
+done

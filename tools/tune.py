@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""Scheduler/option sweep on the C2 workload (manix proxy, 1024^2, 20 it), one
+process, interleaved rounds (cdna_hip_programming.md §5.4 rule 24).
+
+  python tools/tune.py [--rounds 3] [--variants "regenerationSK:ev=16,chunk=128" ...]
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import cudavolumerenderer_amd as cvr  # noqa: E402
+
+DEFAULT = [
+    "naiveSK:",
+    "regenerationSK:sched=1,ev=48,chunk=128",
+    "regenerationSK:ev=16",
+    "regenerationSK:ev=1",
+    "regenerationSK:ev=4",
+    "regenerationSK:ev=32",
+    "regenerationSK:ev=16,pool=1048576",
+    "regenerationSK:ev=16,pool=4194304",
+    "regenerationSK:ev=16,chunk=64",
+    "regenerationSK:ev=16,chunk=512",
+]
+
+
+def parse(v):
+    k, _, opts = v.partition(":")
+    d = {}
+    for kv in filter(None, opts.split(",")):
+        a, b = kv.split("=")
+        d[a] = int(b)
+    return k, d
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--scene", default="manix")
+    ap.add_argument("--variants", nargs="*", default=DEFAULT)
+    a = ap.parse_args()
+    scene = cvr.Scene.synthetic(a.scene)
+    W = H = a.res
+    iv, r2v = cvr.default_camera(W, H)
+    ctxs = []
+    for v in a.variants:
+        k, d = parse(v)
+        c = cvr.Context(0, k)
+        c.set_medium(scene.medium)
+        c.set_camera(iv, r2v, (W, H))
+        if "ev" in d:
+            c.set_option(cvr.OPT_EVENT_THRESHOLD, d["ev"])
+        if "chunk" in d:
+            c.set_option(cvr.OPT_CHUNK, d["chunk"])
+        if "grid" in d:
+            c.set_option(cvr.OPT_GRID, d["grid"])
+        if "sched" in d:
+            c.set_option(cvr.OPT_SCHEDULER, d["sched"])
+        if "pool" in d:
+            c.set_option(cvr.OPT_POOL, d["pool"])
+        c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
+        c.init()
+        c.set_resolution(W, H)
+        c.set_iterations(a.iters)
+        ctxs.append((v, c))
+    times = {v: [] for v, _ in ctxs}
+    extra = {}
+    for r in range(a.rounds + 1):
+        for v, c in ctxs:
+            c.clear_output()
+            t0 = time.perf_counter()
+            c.launch_render()
+            st = c.stats()
+            wall = (time.perf_counter() - t0) * 1e3
+            if r > 0:
+                times[v].append(wall)
+                extra[v] = (st.kernel_ms, st.iterations, st.track_ms, st.events_ms, st.steps, st.escaped)
+    cu, grid = ctxs[-1][1].device_info()
+    print(f"CUs {cu}, persistent grid {grid} blocks; steps/launch {st.steps}, density {st.density}")
+    for v, _ in ctxs:
+        t = np.array(times[v])
+        kms, its, tms, ems, steps, esc = extra[v]
+        gsteps = steps / (np.median(t) * 1e-3) / 1e9
+        print(f"{v:42s} wall {np.median(t):8.3f} ms (min {t.min():7.3f}) dev {kms:8.3f}  it {its:4d} "
+              f"track {tms:7.3f} events {ems:7.3f}  {W * H * a.iters / np.median(t) / 1e3:7.1f} Msamples/s "
+              f"{gsteps:6.2f} Gsteps/s  esc {esc}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
