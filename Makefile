@@ -43,3 +43,10 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean resource-usage
+
+# Diagnostic build with in-kernel phase stamps (never the shipped library).
+stamps: build/stamps/libcvr.so
+build/stamps/libcvr.so: $(SRCS_HIP) $(SRCS_CPP) $(HDRS)
+	@mkdir -p build/stamps
+	$(HIPCC) $(HIPFLAGS) -DCVR_STAMPS=1 -shared -o $@ $(SRCS_HIP) $(patsubst %,-x hip %,$(SRCS_CPP))
+.PHONY: stamps

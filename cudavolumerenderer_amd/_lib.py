@@ -26,7 +26,7 @@ NAIVE_SK, NAIVE_MK, REGENERATION_SK, STREAMING_MK, STREAMING_SK, SORTING_SK = ra
 SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4}
 
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
-OPT_SCHEDULER, OPT_POOL, OPT_TIMING = 6, 7, 8
+OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 
 
 class CvrError(RuntimeError):

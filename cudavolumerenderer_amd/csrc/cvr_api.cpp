@@ -50,6 +50,8 @@ struct cvr_ctx {
   // medium in HBM
   float* d_density = nullptr;
   float4* d_albedo = nullptr;
+  float4* d_cells = nullptr;  // corner-replicated density (MediumParams::cells)
+  bool use_cells = true;
   size_t n_voxels = 0;
   bool have_medium = false;
   cvr::MediumParams m{};
@@ -71,12 +73,14 @@ struct cvr_ctx {
   float4* d_out = nullptr;  // active output (owned or external)
   bool external_out = false;
 
-  unsigned char* d_work = nullptr;  // queue head + stats counters
+  unsigned char* d_work = nullptr;  // queue heads + stats counters (kWork* layout)
+  uint32_t n_queues = 8;            // work-order bands (one per XCD)
+  int order = 1;                    // 1: pixel-block/sample-inner order when the launch allows it
 
   // options
   uint32_t max_segments = 1u << 20;
-  uint32_t chunk = 128;
-  uint32_t ev_thresh = 16;
+  uint32_t chunk = 256;
+  uint32_t ev_thresh = 56;
   uint32_t grid_override = 0;
   int scatter_eps = -1;
 
@@ -84,7 +88,8 @@ struct cvr_ctx {
   int persistent_grid = 0;
   int track_grid = 0;
   bool inited = false;
-  int scheduler = 0;  // 0 wavefront (default), 1 single persistent kernel
+  int scheduler = 0;  // 0 single persistent kernel (default), 1 wavefront kernel pair
+  int waves = 4;      // persistent kernel register budget (waves per SIMD)
 
   // wavefront pool (cvr_wavefront.hip)
   unsigned char* d_pool = nullptr;
@@ -101,7 +106,12 @@ struct cvr_ctx {
   cvr_stats last{};
 };
 
-#define HIP_TRY(ctx, expr)                                                                              \
+// d_work layout: 8 queue heads one 64-byte line apart, then 16 u64 stats
+// (single-kernel launches / wavefront events, wavefront track), then 8 u64
+// diagnostic counters (CVR_STAMPS builds).
+constexpr size_t kWorkQueues = 0, kWorkStats = 512, kWorkDebug = 640, kWorkBytes = 1024;
+
+#define HIP_TRY(ctx, expr)                                                                         \
   do {                                                                                                  \
     hipError_t e_ = (expr);                                                                             \
     if (e_ != hipSuccess)                                                                               \
@@ -157,10 +167,27 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   L.seed_base = c->seed;
   L.max_segments = c->max_segments;
   L.out = c->d_out;
-  L.queue = reinterpret_cast<unsigned int*>(c->d_work);
-  L.stats = reinterpret_cast<unsigned long long*>(c->d_work + 64);
-  L.chunk = c->chunk ? c->chunk : 128;
+  L.queue = reinterpret_cast<unsigned int*>(c->d_work + kWorkQueues);
+  L.stats = reinterpret_cast<unsigned long long*>(c->d_work + kWorkStats);
+  L.chunk = c->chunk ? c->chunk : 256;
   L.ev_thresh = c->ev_thresh ? c->ev_thresh : 1;
+  // work order (see LaunchParams): pixel blocks with samples innermost, one
+  // contiguous band of blocks per queue, when the launch covers whole samples
+  const uint64_t P = L.tile_px;
+  const bool aligned = P && first % P == 0 && count % P == 0 && count > 0;
+  if (c->order && aligned && c->tile_w % 8 == 0 && c->tile_h % 8 == 0) {
+    L.order = 1;
+    L.samples = (uint32_t)(count / P);
+    L.blocks_x = c->tile_w / 8;
+    L.n_blocks = (uint32_t)(P / 64);
+    L.n_queues = c->n_queues < L.n_blocks ? c->n_queues : L.n_blocks;
+  } else {
+    L.order = 0;
+    L.samples = 0;
+    L.blocks_x = 0;
+    L.n_blocks = 0;
+    L.n_queues = 1;
+  }
 }
 
 int check_ready(cvr_ctx* c) {
@@ -178,7 +205,7 @@ int do_init(cvr_ctx* c) {
   HIP_TRY(c, hipGetDeviceProperties(&prop, c->device));
   c->cu_count = prop.multiProcessorCount;
   int bpc = 0;
-  HIP_TRY(c, cvr::persistent_occupancy(scatter_eps_for(c), &bpc));
+  HIP_TRY(c, cvr::persistent_occupancy(scatter_eps_for(c), c->waves, &bpc));
   if (bpc < 1) bpc = 1;
   c->persistent_grid = bpc * c->cu_count;
   int tbpc = 0;
@@ -282,7 +309,7 @@ int wf_render(cvr_ctx* c, const cvr::LaunchParams& L, bool eps) {
     track_ms += b;
   }
   // fold the per-wave counters into the context's 8 stats words
-  unsigned long long* stats = reinterpret_cast<unsigned long long*>(c->d_work + 64);
+  unsigned long long* stats = reinterpret_cast<unsigned long long*>(c->d_work + kWorkStats);
   HIP_TRY(c, cvr::wf_launch_reduce(P.stats_events, ev_waves, stats, s));
   HIP_TRY(c, cvr::wf_launch_reduce(P.stats_track, tr_waves, stats + 8, s));
   c->last_iterations = it;
@@ -336,9 +363,9 @@ int cvr_create(int device, int kernel, cvr_ctx** out) {
   c->stream = c->own_stream;
   if ((e = hipEventCreate(&c->ev_start)) != hipSuccess) return fail("hipEventCreate", e);
   if ((e = hipEventCreate(&c->ev_stop)) != hipSuccess) return fail("hipEventCreate", e);
-  if ((e = hipMalloc(&c->d_work, 256)) != hipSuccess) return fail("hipMalloc(work)", e);
+  if ((e = hipMalloc(&c->d_work, kWorkBytes)) != hipSuccess) return fail("hipMalloc(work)", e);
   // stats words: [64,128) single-kernel launches / wavefront events, [128,192) wavefront track
-  if ((e = hipMemset(c->d_work, 0, 256)) != hipSuccess) return fail("hipMemset(work)", e);
+  if ((e = hipMemset(c->d_work, 0, kWorkBytes)) != hipSuccess) return fail("hipMemset(work)", e);
   *out = c;
   return CVR_OK;
 }
@@ -349,6 +376,7 @@ int cvr_destroy(cvr_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->d_density) (void)hipFree(c->d_density);
   if (c->d_albedo) (void)hipFree(c->d_albedo);
+  if (c->d_cells) (void)hipFree(c->d_cells);
   if (c->d_out_owned) (void)hipFree(c->d_out_owned);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -381,12 +409,23 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   }
   HIP_TRY(c, hipMemcpy(c->d_density, md->density, n * sizeof(float), hipMemcpyHostToDevice));
   HIP_TRY(c, hipMemcpy(c->d_albedo, md->albedo, n * sizeof(float4), hipMemcpyHostToDevice));
+  if (c->d_cells) (void)hipFree(c->d_cells);
+  c->d_cells = nullptr;
+  if (c->use_cells) {
+    HIP_TRY(c, hipMalloc(&c->d_cells, 2 * n * sizeof(float4)));
+    HIP_TRY(c, cvr::launch_build_cells(c->d_density, md->res[0], md->res[1], md->res[2], c->d_cells, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
   cvr::MediumParams& m = c->m;
+  m.cells = c->d_cells;
   m.density = c->d_density;
   m.albedo = c->d_albedo;
   m.rx = md->res[0];
   m.ry = md->res[1];
   m.rz = md->res[2];
+  m.fres_x = (float)md->res[0];
+  m.fres_y = (float)md->res[1];
+  m.fres_z = (float)md->res[2];
   m.gx = (float)(md->res[0] - 1u);
   m.gy = (float)(md->res[1] - 1u);
   m.gz = (float)(md->res[2] - 1u);
@@ -517,6 +556,23 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
     case CVR_OPT_TIMING:
       c->wf_timing = v != 0;
       return CVR_OK;
+    case CVR_OPT_ORDER:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "order must be 0 or 1");
+      c->order = (int)v;
+      return CVR_OK;
+    case CVR_OPT_QUEUES:
+      if (v < 1 || v > 8) return set_err(&c->err, CVR_ERR_INVALID, "queues must be 1..8");
+      c->n_queues = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_WAVES:
+      if (v != 4 && v != 5 && v != 6 && v != 8) return set_err(&c->err, CVR_ERR_INVALID, "waves must be 4, 5, 6 or 8");
+      c->waves = (int)v;
+      c->inited = false;
+      return CVR_OK;
+    case CVR_OPT_CELLS:
+      // takes effect at the next cvr_set_medium
+      c->use_cells = v != 0;
+      return CVR_OK;
     case CVR_OPT_SCATTER_EPS:
       if (v < -1 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "scatter_eps must be -1, 0 or 1");
       c->scatter_eps = (int)v;
@@ -552,15 +608,15 @@ int cvr_launch_render(cvr_ctx* c) {
   cvr::LaunchParams L{};
   fill_launch(c, L, first, count);
   const bool eps = scatter_eps_for(c);
-  HIP_TRY(c, hipMemsetAsync(c->d_work, 0, 192, c->stream));
+  HIP_TRY(c, hipMemsetAsync(c->d_work, 0, kWorkBytes, c->stream));
   HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
   c->last_iterations = 0;
   c->last_track_ms = c->last_events_ms = 0;
   if (c->kernel == CVR_KERNEL_NAIVE_SK) {
     HIP_TRY(c, cvr::launch_naive(c->m, L, eps, c->stream));
-  } else if (c->scheduler == 1) {
+  } else if (c->scheduler == 0) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
-    HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, grid, c->stream));
+    HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, c->waves, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }
@@ -595,7 +651,7 @@ int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   if (!c || !st) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   unsigned long long w[16] = {0};
-  HIP_TRY(c, hipMemcpy(w, c->d_work + 64, sizeof(w), hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(w, c->d_work + kWorkStats, sizeof(w), hipMemcpyDeviceToHost));
   unsigned long long v[8];
   for (int k = 0; k < 8; ++k) v[k] = w[k] + w[8 + k];  // wavefront: events + track rows
   cvr_stats s{};
@@ -617,6 +673,13 @@ int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   s.events_ms = c->last_events_ms;
   *st = s;
   c->last = s;
+  return CVR_OK;
+}
+
+int cvr_debug_counters(cvr_ctx* c, uint64_t out[8]) {
+  if (!c || !out) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(out, c->d_work + kWorkDebug, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return CVR_OK;
 }
 

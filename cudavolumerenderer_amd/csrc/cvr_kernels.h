@@ -39,11 +39,13 @@ hipError_t wf_track_occupancy(int* blocks_per_cu);
 hipError_t wf_launch_reduce(const unsigned long long* rows, uint32_t nrows, unsigned long long* out, hipStream_t s);
 
 hipError_t launch_naive(const MediumParams& m, const LaunchParams& L, bool scatter_eps, hipStream_t s);
-hipError_t launch_persistent(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
-                             hipStream_t s);
-hipError_t persistent_occupancy(bool scatter_eps, int* blocks_per_cu);
+hipError_t launch_persistent(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves,
+                             uint32_t grid, hipStream_t s);
+hipError_t persistent_occupancy(bool scatter_eps, int waves, int* blocks_per_cu);
 hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatter_eps, PathRecord* rec,
                         hipStream_t s);
+hipError_t launch_build_cells(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, float4* cells,
+                              hipStream_t s);
 hipError_t launch_tile_to_image(const float4* tile, uint32_t tw, uint32_t th, float4* image, uint32_t iw,
                                 uint32_t ox, uint32_t oy, float scale, hipStream_t s);
 

@@ -72,8 +72,16 @@ CVR_DEV float rng_float(Rng& s) {
 // ------------------------------------------------------ kernel params -----
 struct MediumParams {
   const float* __restrict__ density;  // rx*ry*rz fp32, x fastest
+  // Corner-replicated copy of the density for the Woodcock gathers: cell
+  // (x,y,z) holds its 8 trilinear corners (texel-clamped as the reference's
+  // point-sampled texture) in two float4 = 32 contiguous bytes, so one
+  // evaluation is 2 x 16-byte loads from one cache line instead of 8 scattered
+  // dword gathers.  Cells exist for 0 <= x1 < rx etc.; other corners (the Q5
+  // uint wrap at -1, far out-of-range taps) use `density`.
+  const float4* __restrict__ cells;   // 2 * rx*ry*rz float4, may be null
   const float4* __restrict__ albedo;  // rx*ry*rz float4 (rgb, w=1)
   uint32_t rx, ry, rz;
+  float fres_x, fres_y, fres_z;  // (float)res
   float gx, gy, gz;  // (float)(res-1): DeviceVolume::volumeToGrid
   V3 bmin, bmax;
   V3 shift;          // box_min / extent  (worldToAABB precedence, Q4)
@@ -97,11 +105,40 @@ struct LaunchParams {
   uint32_t seed_base;     // RNG seed = seed_base + path_id
   uint32_t max_segments;  // safety cap (0 = none)
   float4* out;            // tile accumulator, tile_px float4
-  unsigned int* queue;    // [0] work-queue head (zeroed per launch)
+  unsigned int* queue;    // work-queue heads, one per 64-byte line (zeroed per launch)
   unsigned long long* stats;  // CVR_STAT_* counters (zeroed per launch)
   uint32_t chunk;         // paths per wave dequeue
   uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
+  // Work order (scheduling only; results are bound to path ids).  order 0:
+  // path ids in sample-major order from one queue.  order 1: 8x8-pixel
+  // blocks with all their samples back to back (path_first must be a
+  // multiple of tile_px, path_count = samples * tile_px, tile dims multiples
+  // of 8); the block range is split into n_queues contiguous bands, one
+  // queue each, so that the waves of one XCD share one band (its L2).
+  uint32_t order;
+  uint32_t samples;       // path_count / tile_px (order 1)
+  uint32_t blocks_x;      // tile_w / 8
+  uint32_t n_blocks;      // tile_px / 64
+  uint32_t n_queues;      // 1..8
 };
+
+// Map the u-th work unit of queue q to a path id (order 1), see LaunchParams.
+CVR_DEV uint32_t queue_blocks_begin(const LaunchParams& L, uint32_t q) {
+  return (uint32_t)(((unsigned long long)L.n_blocks * q) / L.n_queues);
+}
+CVR_DEV uint32_t queue_units(const LaunchParams& L, uint32_t q) {
+  if (L.order == 0) return q == 0 ? L.path_count : 0u;
+  return (queue_blocks_begin(L, q + 1) - queue_blocks_begin(L, q)) * 64u * L.samples;
+}
+CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
+  if (L.order == 0) return L.path_first + u;
+  const uint32_t per_block = 64u * L.samples;
+  const uint32_t b = queue_blocks_begin(L, q) + u / per_block;
+  const uint32_t rem = u % per_block;
+  const uint32_t s = rem >> 6, lane = rem & 63u;
+  const uint32_t px = (b % L.blocks_x) * 8u + (lane & 7u), py = (b / L.blocks_x) * 8u + (lane >> 3);
+  return L.path_first + s * L.tile_px + py * L.tile_w + px;
+}
 
 enum {
   STAT_PATHS = 0,
@@ -142,7 +179,35 @@ CVR_DEV Tri tri_setup(const MediumParams& m, V3 p) {
   t.zb = texel(z1 + 1, m.rz);
   return t;
 }
+CVR_DEV float trilerp8(float d000, float d001, float d010, float d011, float d100, float d101, float d110,
+                       float d111, float fx, float fy, float fz) {
+  const float _fx = 1.0f - fx, _fy = 1.0f - fy, _fz = 1.0f - fz;
+  const float a = lerpf(lerpf(d000, d001, fx, _fx), lerpf(d010, d011, fx, _fx), fy, _fy);
+  const float b = lerpf(lerpf(d100, d101, fx, _fx), lerpf(d110, d111, fx, _fx), fy, _fy);
+  return lerpf(a, b, fz, _fz);
+}
+
+CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p);
+
+// Woodcock density evaluation: cell path when the lower corner is inside the
+// grid (the overwhelmingly common case), else the 8-tap gather.
 CVR_DEV float density_lookup(const MediumParams& m, V3 p) {
+  if (m.cells) {
+    const float cx = p.x * m.gx, cy = p.y * m.gy, cz = p.z * m.gz;
+    // floor in float; for 0 <= f < res the int conversion is exact, so this
+    // equals det_floor_i32 + the uint range test (NaN fails the test).
+    const float fx1 = __builtin_floorf(cx), fy1 = __builtin_floorf(cy), fz1 = __builtin_floorf(cz);
+    if (fx1 >= 0.0f && fx1 < m.fres_x && fy1 >= 0.0f && fy1 < m.fres_y && fz1 >= 0.0f && fz1 < m.fres_z) {
+      const uint32_t x1 = (uint32_t)fx1, y1 = (uint32_t)fy1, z1 = (uint32_t)fz1;
+      const uint32_t cell = (__umul24(z1, m.ry) + y1) * m.rx + x1;
+      const float4 lo = m.cells[2 * cell], hi = m.cells[2 * cell + 1];
+      return trilerp8(lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, cx - fx1, cy - fy1, cz - fz1);
+    }
+  }
+  return density_lookup_gather(m, p);
+}
+
+CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p) {
   const Tri t = tri_setup(m, p);
   const float* __restrict__ D = m.density;
   const uint32_t r00 = (t.za * m.ry + t.ya) * m.rx, r01 = (t.za * m.ry + t.yb) * m.rx;
@@ -209,7 +274,9 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
                           uint32_t& n_steps, uint32_t& n_density) {
   const float xi = rng_float(rng);
-  t = det_fmaf(-det_logf(det_fmaxf(xi, CVR_EPSILON_F)), m.inv_sigma, t);
+  // == det_logf(det_fmaxf(xi, EPSILON)): xi is never NaN and the clamped
+  // argument is a normal float, so the NaN and subnormal paths are dropped.
+  t = det_fmaf(-det_logf_normal(xi < CVR_EPSILON_F ? CVR_EPSILON_F : xi), m.inv_sigma, t);
   ++n_steps;
   if (!(t <= max_t)) return 1;
   const V3 p = mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z));

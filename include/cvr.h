@@ -63,9 +63,14 @@ typedef enum {
   CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
   CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
   CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
-  CVR_OPT_SCHEDULER = 6,      /* persistent kernels: 0 wavefront (default), 1 single kernel */
+  CVR_OPT_SCHEDULER = 6,      /* regenerationSK: 0 single persistent kernel (default), 1 wavefront pair */
   CVR_OPT_POOL = 7,           /* wavefront ray-slot pool size (default 2^21) */
-  CVR_OPT_TIMING = 8          /* 1: time every wavefront kernel (track_ms / events_ms) */
+  CVR_OPT_TIMING = 8,         /* 1: time every wavefront kernel (track_ms / events_ms) */
+  CVR_OPT_CELLS = 9           /* 1 (default): corner-replicated density cells (8x density bytes
+                                 in HBM, 2 x 16 B loads per Woodcock step); applies at set_medium */,
+  CVR_OPT_WAVES = 10,         /* persistent kernel register budget: 4 (default), 5, 6, 8 waves/SIMD */
+  CVR_OPT_ORDER = 11,         /* 1 (default): 8x8-pixel blocks, samples innermost; 0: path-id order */
+  CVR_OPT_QUEUES = 12         /* work bands / queues, one per XCD (default 8) */
 } cvr_option;
 
 /* HeterogeneousMedium + GGX boundary (Medium.h:110-190, Bsdf.h:17-30). */
@@ -158,6 +163,10 @@ int cvr_copy_output(cvr_ctx* ctx, float* host_rgba, float scale);
 /* Debug/parity: trace path ids [first, first+count) one per work-item and
  * return per-path records (no framebuffer splat). */
 int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_record* host_out);
+/* Diagnostic builds (-DCVR_STAMPS=1) only: per-phase cycle counters of the
+ * persistent kernel {event cycles, track cycles, event phases, track
+ * iterations}, summed over waves; zeros otherwise. */
+int cvr_debug_counters(cvr_ctx* ctx, uint64_t out[8]);
 /* Device properties used for sizing: CU count, persistent grid. */
 int cvr_device_info(cvr_ctx* ctx, int* cu_count, int* persistent_grid);
 

@@ -68,14 +68,7 @@ CVR_HD int det_floor_i32(float x) {
 }
 
 /* ---------------------------------------------------------------- log --- */
-CVR_HD float det_logf(float x) {
-  uint32_t ix = det_f2u(x);
-  int k = 0;
-  if (ix < 0x00800000u) { /* subnormal (x > 0 assumed) */
-    x *= 33554432.0f;     /* 2^25 */
-    ix = det_f2u(x);
-    k = -25;
-  }
+CVR_HD float det_logf_core(uint32_t ix, int k) {
   /* reduce x into [sqrt(2)/2, sqrt(2)) */
   ix += 0x3f800000u - 0x3f3504f3u;
   k += (int)(ix >> 23) - 0x7f;
@@ -97,6 +90,18 @@ CVR_HD float det_logf(float x) {
   y = y + f;
   return det_fmaf(dk, 0.6931381225585938f, y);
 }
+/* log(x) for x > 0 (normal or subnormal). */
+CVR_HD float det_logf(float x) {
+  uint32_t ix = det_f2u(x);
+  int k = 0;
+  if (ix < 0x00800000u) { /* subnormal: scale by 2^25 */
+    ix = det_f2u(x * 33554432.0f);
+    k = -25;
+  }
+  return det_logf_core(ix, k);
+}
+/* Same result as det_logf for normal x > 0. */
+CVR_HD float det_logf_normal(float x) { return det_logf_core(det_f2u(x), 0); }
 
 /* ------------------------------------------------------------ sin/cos --- */
 CVR_HD float det_sin_poly(float r, float z) {

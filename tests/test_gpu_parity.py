@@ -17,8 +17,9 @@ pytestmark = pytest.mark.gpu
 NTHREADS = min(16, os.cpu_count() or 1)
 
 
-def make_ctx(cvr, scene, W, H, kernel, seed=0):
+def make_ctx(cvr, scene, W, H, kernel, seed=0, cells=1):
     ctx = cvr.Context(0, kernel)
+    ctx.set_option(cvr.OPT_CELLS, cells)
     ctx.set_medium(scene.medium)
     iv, r2v = cvr.default_camera(W, H)
     ctx.set_camera(iv, r2v, (W, H))
@@ -76,11 +77,12 @@ def scenes(cvr):
 
 @pytest.mark.parametrize("scene_key", list(SCENES))
 @pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
-def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel):
+@pytest.mark.parametrize("cells", [1, 0])
+def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel, cells):
     scene = scenes[scene_key]
     W = H = 64
     iters = 3
-    ctx, iv, r2v = make_ctx(cvr, scene, W, H, kernel, seed=7)
+    ctx, iv, r2v = make_ctx(cvr, scene, W, H, kernel, seed=7, cells=cells)
     ctx.set_resolution(W, H)
     ctx.set_iterations(iters)
     n = W * H * iters
@@ -128,15 +130,20 @@ def test_scheduler_knobs_do_not_change_results(cvr, scenes):
     # (chunk, event/refill threshold, grid, scheduler, pool): the single
     # persistent kernel and the wavefront scheduler with pools from 256 slots
     # (hundreds of events/track iterations) up must all give the same result.
-    for chunk, thresh, grid, sched, pool in [(128, 16, 0, 0, 1 << 21), (64, 1, 0, 0, 256), (256, 64, 0, 0, 4096),
-                                             (32, 8, 7, 0, 1000), (128, 16, 0, 1, 1 << 21), (64, 1, 0, 1, 1 << 21),
-                                             (256, 64, 0, 1, 1 << 21), (32, 8, 7, 1, 1 << 21)]:
+    # sched 0 = persistent kernel (with work orders/queues), 1 = wavefront pair
+    for chunk, thresh, grid, sched, pool, order, queues in [
+            (128, 56, 0, 0, 1 << 21, 1, 8), (128, 16, 0, 0, 1 << 21, 0, 1), (64, 1, 0, 0, 1 << 21, 1, 3),
+            (256, 64, 0, 0, 1 << 21, 1, 1), (32, 8, 7, 0, 1 << 21, 1, 8), (100, 30, 3, 0, 1 << 21, 0, 1),
+            (128, 16, 0, 1, 1 << 21, 1, 8), (64, 1, 0, 1, 256, 1, 8), (256, 64, 0, 1, 4096, 1, 8),
+            (32, 8, 7, 1, 1000, 1, 8)]:
         ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
         ctx.set_option(cvr.OPT_CHUNK, chunk)
         ctx.set_option(cvr.OPT_EVENT_THRESHOLD, thresh)
         ctx.set_option(cvr.OPT_GRID, grid)
         ctx.set_option(cvr.OPT_SCHEDULER, sched)
         ctx.set_option(cvr.OPT_POOL, pool)
+        ctx.set_option(cvr.OPT_ORDER, order)
+        ctx.set_option(cvr.OPT_QUEUES, queues)
         img, st = ctx.render_image(W, H, (1, 1), 4)
         key = (st.paths, st.segments, st.steps, st.density, st.albedo, st.escaped)
         if base is None:

@@ -18,15 +18,16 @@ import cudavolumerenderer_amd as cvr  # noqa: E402
 
 DEFAULT = [
     "naiveSK:",
-    "regenerationSK:sched=1,ev=48,chunk=128",
-    "regenerationSK:ev=16",
-    "regenerationSK:ev=1",
-    "regenerationSK:ev=4",
-    "regenerationSK:ev=32",
-    "regenerationSK:ev=16,pool=1048576",
-    "regenerationSK:ev=16,pool=4194304",
-    "regenerationSK:ev=16,chunk=64",
-    "regenerationSK:ev=16,chunk=512",
+    "regenerationSK:order=0,queues=1",
+    "regenerationSK:order=0",
+    "regenerationSK:",
+    "regenerationSK:queues=1",
+    "regenerationSK:chunk=64",
+    "regenerationSK:chunk=256",
+    "regenerationSK:ev=48",
+    "regenerationSK:ev=60",
+    "regenerationSK:cells=0",
+    "regenerationSK:cells=0,ev=48",
 ]
 
 
@@ -54,6 +55,7 @@ def main():
     for v in a.variants:
         k, d = parse(v)
         c = cvr.Context(0, k)
+        c.set_option(cvr.OPT_CELLS, d.get("cells", 1))
         c.set_medium(scene.medium)
         c.set_camera(iv, r2v, (W, H))
         if "ev" in d:
@@ -64,6 +66,12 @@ def main():
             c.set_option(cvr.OPT_GRID, d["grid"])
         if "sched" in d:
             c.set_option(cvr.OPT_SCHEDULER, d["sched"])
+        if "order" in d:
+            c.set_option(cvr.OPT_ORDER, d["order"])
+        if "queues" in d:
+            c.set_option(cvr.OPT_QUEUES, d["queues"])
+        if "waves" in d:
+            c.set_option(cvr.OPT_WAVES, d["waves"])
         if "pool" in d:
             c.set_option(cvr.OPT_POOL, d["pool"])
         c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
