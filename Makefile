@@ -11,7 +11,7 @@ CSRC := $(PKG)/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 OBJDIR := build/obj
-SRCS_HIP := $(CSRC)/cvr_kernels.hip $(CSRC)/cvr_wavefront.hip
+SRCS_HIP := $(CSRC)/cvr_kernels.hip $(CSRC)/cvr_persistent.hip $(CSRC)/cvr_wavefront.hip
 SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := include/cvr.h include/cvr_detmath.h $(wildcard $(CSRC)/*.h)
@@ -36,7 +36,7 @@ oracle:
 	$(MAKE) -C oracle
 
 resource-usage:
-	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $(CSRC)/cvr_kernels.hip -o /dev/null
+	for f in $(SRCS_HIP); do $(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $$f -o /dev/null; done
 
 clean:
 	rm -rf build $(PKG)/libcvr.so $(PKG)/cvr

@@ -565,7 +565,8 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->n_queues = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_WAVES:
-      if (v != 4 && v != 5 && v != 6 && v != 8) return set_err(&c->err, CVR_ERR_INVALID, "waves must be 4, 5, 6 or 8");
+      if (v != 3 && v != 4 && v != 5 && v != 6 && v != 8)
+        return set_err(&c->err, CVR_ERR_INVALID, "waves must be 3, 4, 5, 6 or 8");
       c->waves = (int)v;
       c->inited = false;
       return CVR_OK;

@@ -18,16 +18,13 @@ import cudavolumerenderer_amd as cvr  # noqa: E402
 
 DEFAULT = [
     "naiveSK:",
-    "regenerationSK:order=0,queues=1",
-    "regenerationSK:order=0",
     "regenerationSK:",
-    "regenerationSK:queues=1",
-    "regenerationSK:chunk=64",
-    "regenerationSK:chunk=256",
+    "regenerationSK:waves=3",
+    "regenerationSK:waves=3,ev=48",
+    "regenerationSK:waves=3,ev=60",
     "regenerationSK:ev=48",
-    "regenerationSK:ev=60",
-    "regenerationSK:cells=0",
-    "regenerationSK:cells=0,ev=48",
+    "regenerationSK:chunk=512",
+    "regenerationSK:waves=3,chunk=512",
 ]
 
 
