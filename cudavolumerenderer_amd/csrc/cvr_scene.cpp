@@ -20,36 +20,25 @@ namespace cvr {
 
 // -------------------------------------------------------------- Raw -------
 // RawSceneBuilder::getAlbedoFromDensity (RawSceneBuilder.h:95-140)
+// The table is two colour ramps, green->red over 20 entries then red->blue
+// over 80; entry i of a ramp is a + i*(b - a)/100 (fp32, that operation
+// order), alpha 1.  A voxel takes entry ceil(density * 99).
+static void tf_ramp(std::vector<float>& tf, const float (&a)[3], const float (&b)[3], int entries) {
+  for (int i = 0; i < entries; ++i) {
+    for (int c = 0; c < 3; ++c) tf.push_back(a[c] + ((float)i * (b[c] - a[c]) / 100.F));
+    tf.push_back(1.F);
+  }
+}
+
 static std::vector<float> raw_transfer_albedo(const std::vector<float>& density) {
-  const float func_length = 100.F;
-  std::vector<float> tf;  // rgba entries
-  float start_r = 0.02f, start_g = 0.2f, start_b = 0.02f;
-  float end_r = 1.F, end_g = 0.02f, end_b = 0.02f;
-  for (int i = 0; i < func_length * 1.F / 5.F; i++) {
-    tf.push_back(start_r + (i * (end_r - start_r) / func_length));
-    tf.push_back(start_g + (i * (end_g - start_g) / func_length));
-    tf.push_back(start_b + (i * (end_b - start_b) / func_length));
-    tf.push_back(1.F);
-  }
-  start_r = end_r;
-  start_g = end_g;
-  start_b = end_b;
-  end_r = 0.0F;
-  end_g = 0.02f;
-  end_b = 1.0f;
-  for (int i = 0; i < func_length * 4.F / 5.F; i++) {
-    tf.push_back(start_r + (i * (end_r - start_r) / func_length));
-    tf.push_back(start_g + (i * (end_g - start_g) / func_length));
-    tf.push_back(start_b + (i * (end_b - start_b) / func_length));
-    tf.push_back(1.F);
-  }
-  const size_t n_tf = tf.size() / 4;
+  static const float green[3] = {0.02f, 0.2f, 0.02f}, red[3] = {1.F, 0.02f, 0.02f}, blue[3] = {0.F, 0.02f, 1.F};
+  std::vector<float> tf;
+  tf_ramp(tf, green, red, 20);
+  tf_ramp(tf, red, blue, 80);
+  const float last = (float)(tf.size() / 4 - 1);
   std::vector<float> albedo(density.size() * 4);
-  for (size_t i = 0; i < density.size(); i++) {
-    const float v = density[i] * (float)(n_tf - 1);
-    const size_t k = (size_t)std::ceil(v);
-    memcpy(&albedo[4 * i], &tf[4 * k], 4 * sizeof(float));
-  }
+  for (size_t i = 0; i < density.size(); ++i)
+    memcpy(&albedo[4 * i], &tf[4 * (size_t)std::ceil(density[i] * last)], 4 * sizeof(float));
   return albedo;
 }
 
@@ -365,7 +354,8 @@ int cvr_write_hdr(const char* path, const float* rgba, uint32_t w, uint32_t h) {
       const float* px = rgba + ((size_t)y * w + x) * 4;
       unsigned char* e = &line[(size_t)x * 4];
       const float mx = std::max(px[0], std::max(px[1], px[2]));
-      if (mx < 1e-32f) {
+      if (!(mx >= 1e-32f) || !std::isfinite(mx) || px[0] != px[0] || px[1] != px[1] || px[2] != px[2]) {
+        // black for empty, negative and non-finite pixels (quirk Q22 NaNs)
         e[0] = e[1] = e[2] = e[3] = 0;
       } else {
         int ex;

@@ -1,0 +1,90 @@
+"""Multi-rank path on CPU: world_size 2 over gloo.
+
+The GPU ranks render a contiguous path-id shard each and sum the framebuffer
+with one all-reduce (cudavolumerenderer_amd/distributed.py).  Here the
+per-rank renderer is the CPU oracle (test infrastructure, standing in for
+the HIP kernel that -m gpu tests cover), so the test checks the sharding and
+the reduction: the 2-rank sum equals the 1-rank render up to fp32
+summation order, and the counters add up exactly.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cudavolumerenderer_amd.distributed import render_sharded, shard_range
+
+W = H = 24
+ITERS = 3
+
+
+@pytest.mark.parametrize("n,world", [(10, 3), (7, 8), (0, 2), (1 << 20, 8), (12345, 1)])
+def test_shard_range_partitions(n, world):
+    seen = 0
+    sizes = []
+    for r in range(world):
+        a, c = shard_range(n, r, world)
+        assert a == seen
+        seen += c
+        sizes.append(c)
+    assert seen == n and max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_range(n, world, world)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _scene_and_launch():
+    import cudavolumerenderer_amd as cvr
+    import oracle
+    s = cvr.Scene.synthetic("bucky")
+    orc = oracle.Oracle.from_medium_desc(s.medium, s.density, s.albedo)
+    iv, r2v = cvr.default_camera(W, H)
+    L = orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 2, 0)
+    return orc, L
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        orc, L = _scene_and_launch()
+        stats = {}
+
+        def render_range(first, count):
+            img, st = orc.render(L, first, count, nthreads=2)
+            stats.update(st.as_dict())
+            return torch.from_numpy(img)
+
+        acc = render_sharded(render_range, W * H * ITERS, rank, world, lambda t: dist.all_reduce(t))
+        counts = torch.tensor([stats["steps"], stats["escaped"], stats["paths"]], dtype=torch.int64)
+        dist.all_reduce(counts)
+        if rank == 0:
+            np.save(os.path.join(outdir, "img.npy"), acc.numpy())
+            np.save(os.path.join(outdir, "counts.npy"), counts.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_render_equals_single(tmp_path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert os.path.join(root, "oracle") in sys.path
+    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True, start_method="fork")
+    img = np.load(tmp_path / "img.npy")
+    counts = np.load(tmp_path / "counts.npy")
+    orc, L = _scene_and_launch()
+    ref, st = orc.render(L, 0, W * H * ITERS, nthreads=2)
+    assert tuple(counts) == (st.steps, st.escaped, st.paths)
+    bound = 2 * ITERS * 2.0 ** -24 * np.maximum(np.abs(img), np.abs(ref)) + 1e-30
+    assert (np.abs(img[..., :3] - ref[..., :3]) <= bound[..., :3]).all()
