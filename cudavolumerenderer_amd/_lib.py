@@ -27,6 +27,7 @@ SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4}
 
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
+OPT_BOUNDS = 13
 
 
 class CvrError(RuntimeError):
@@ -46,7 +47,7 @@ class Stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("steps", C.c_uint64),
                 ("density", C.c_uint64), ("albedo", C.c_uint64), ("escaped", C.c_uint64),
                 ("truncated", C.c_uint64), ("kernel_ms", C.c_double), ("iterations", C.c_uint64),
-                ("track_ms", C.c_double), ("events_ms", C.c_double)]
+                ("track_ms", C.c_double), ("events_ms", C.c_double), ("fetches", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -52,6 +52,8 @@ struct cvr_ctx {
   float4* d_albedo = nullptr;
   float4* d_cells = nullptr;  // corner-replicated density (MediumParams::cells)
   bool use_cells = true;
+  uint8_t* d_bounds = nullptr;  // brick bounds (MediumParams::bounds)
+  uint32_t bound_shift = 2;     // log2 brick size, 0 = off
   size_t n_voxels = 0;
   bool have_medium = false;
   cvr::MediumParams m{};
@@ -416,7 +418,26 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
     HIP_TRY(c, cvr::launch_build_cells(c->d_density, md->res[0], md->res[1], md->res[2], c->d_cells, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
+  if (c->d_bounds) (void)hipFree(c->d_bounds);
+  c->d_bounds = nullptr;
+  const float sigma = md->scale * md->max_density;
+  uint32_t bnx = 0, bny = 0;
+  if (c->bound_shift && sigma > 0.0f && std::isfinite(sigma) && md->scale > 0.0f) {
+    const uint32_t B = 1u << c->bound_shift;
+    bnx = (md->res[0] + B - 1) / B;
+    bny = (md->res[1] + B - 1) / B;
+    const size_t nb = (size_t)bnx * bny * ((md->res[2] + B - 1) / B);
+    HIP_TRY(c, hipMalloc(&c->d_bounds, nb));
+    HIP_TRY(c, cvr::launch_build_bounds(c->d_density, md->res[0], md->res[1], md->res[2], c->bound_shift,
+                                        md->max_density, c->d_bounds, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
   cvr::MediumParams& m = c->m;
+  m.bounds = c->d_bounds;
+  m.bshift = c->bound_shift;
+  m.bnx = bnx;
+  m.bny = bny;
+  m.bq = (float)((1.0 / 254.0) * (1.0 + 1.0 / 65536.0));
   m.cells = c->d_cells;
   m.density = c->d_density;
   m.albedo = c->d_albedo;
@@ -570,6 +591,11 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->waves = (int)v;
       c->inited = false;
       return CVR_OK;
+    case CVR_OPT_BOUNDS:
+      // takes effect at the next cvr_set_medium
+      if (v < 0 || v > 5) return set_err(&c->err, CVR_ERR_INVALID, "bounds must be 0 (off) or log2 brick size 1..5");
+      c->bound_shift = (uint32_t)v;
+      return CVR_OK;
     case CVR_OPT_CELLS:
       // takes effect at the next cvr_set_medium
       c->use_cells = v != 0;
@@ -663,6 +689,7 @@ int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   s.albedo = v[cvr::STAT_ALBEDO];
   s.escaped = v[cvr::STAT_ESCAPED];
   s.truncated = v[cvr::STAT_TRUNCATED];
+  s.fetches = v[cvr::STAT_FETCH];
   s.kernel_ms = 0.0;
   if (c->timed) {
     float ms = 0.f;
@@ -756,6 +783,7 @@ int cvr_render_image(cvr_ctx* c, const cvr_render_desc* d, void* device_image, f
     acc.albedo += s.albedo;
     acc.escaped += s.escaped;
     acc.truncated += s.truncated;
+    acc.fetches += s.fetches;
     acc.kernel_ms += s.kernel_ms;
     if ((r = cvr_reset(c))) goto done;  // prepareForNextIterations
     if (ntiles != 1 && (r = cvr_clear_output(c))) goto done;

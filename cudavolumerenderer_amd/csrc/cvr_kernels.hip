@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void k_naive(MediumParams m, LaunchParams L) {
       if (is.inside) {
         int r;
         do {
-          r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY]);
+          r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
         } while (r == 0);
         collided = t < is.dist;
       }
@@ -83,6 +83,7 @@ __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, P
   is.inside = false;
   PathRecord r = {};
   r.image_id = ps.image_id;
+  uint32_t n_fetch = 0;
   for (;;) {
     if (L.max_segments && r.n_segments >= L.max_segments) {
       r.flags |= 2u;
@@ -98,7 +99,7 @@ __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, P
     if (is.inside) {
       int s;
       do {
-        s = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, r.n_steps, r.n_density);
+        s = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, r.n_steps, r.n_density, n_fetch);
       } while (s == 0);
       collided = t < is.dist;
     }
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, P
   r.T[1] = ps.T.y;
   r.T[2] = ps.T.z;
   rec[tid] = r;
+  if (n_fetch) atomicAdd(L.stats + STAT_FETCH, (unsigned long long)n_fetch);
 }
 
 // ----------------------------------------------------- image transfer -----
@@ -141,6 +143,37 @@ __global__ __launch_bounds__(256) void k_build_cells(const float* __restrict__ D
     auto at = [&](uint32_t a, uint32_t b, uint32_t c) { return D[((size_t)c * ry + b) * rx + a]; };
     cells[2 * i] = make_float4(at(x, y, z), at(xb, y, z), at(x, yb, z), at(xb, yb, z));
     cells[2 * i + 1] = make_float4(at(x, y, zb), at(xb, y, zb), at(x, yb, zb), at(xb, yb, zb));
+  }
+}
+
+// --------------------------------------------------------- brick bounds ---
+// MediumParams::bounds.  One work-item per brick: the max over the voxels
+// its cells interpolate (cells [b*B, b*B+B-1] use voxels up to b*B+B, clamped
+// as texel() clamps), quantised upwards to q/254 of max_density.
+__global__ __launch_bounds__(256) void k_build_bounds(const float* __restrict__ D, uint32_t rx, uint32_t ry,
+                                                      uint32_t rz, uint32_t bshift, uint32_t bnx, uint32_t bny,
+                                                      uint32_t bnz, float max_density, uint8_t* __restrict__ q) {
+  const size_t nb = (size_t)bnx * bny * bnz;
+  const uint32_t B = 1u << bshift;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (size_t)gridDim.x * 256) {
+    const uint32_t bx = (uint32_t)(i % bnx), by = (uint32_t)((i / bnx) % bny), bz = (uint32_t)(i / ((size_t)bnx * bny));
+    const uint32_t x0 = bx * B, y0 = by * B, z0 = bz * B;
+    const uint32_t x1 = min(x0 + B, rx - 1), y1 = min(y0 + B, ry - 1), z1 = min(z0 + B, rz - 1);
+    float mx = 0.0f;
+    bool nan = false;
+    for (uint32_t z = z0; z <= z1; ++z)
+      for (uint32_t y = y0; y <= y1; ++y)
+        for (uint32_t x = x0; x <= x1; ++x) {
+          const float v = D[((size_t)z * ry + y) * rx + x];
+          nan |= !(v == v) || v == __builtin_inff();
+          mx = fmaxf(mx, v);
+        }
+    const double r = (double)mx / (double)max_density;
+    uint32_t v;
+    if (nan || !(r <= 1.0)) v = 255u;  // no bound (Q15: XML densities may exceed the majorant)
+    else if (mx == 0.0f) v = 0u;
+    else v = min(254u, (uint32_t)ceil(r * 254.0 * (1.0 + 1e-6)));
+    q[i] = (uint8_t)v;
   }
 }
 
@@ -172,6 +205,15 @@ hipError_t launch_tile_to_image(const float4* tile, uint32_t tw, uint32_t th, fl
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_tile_to_image, dim3((n + 255u) / 256u), dim3(256), 0, s, tile, tw, th, image, iw, ox, oy,
                      scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
+                               float max_density, uint8_t* bounds, hipStream_t s) {
+  const uint32_t B = 1u << bshift;
+  const uint32_t bnx = (rx + B - 1) / B, bny = (ry + B - 1) / B, bnz = (rz + B - 1) / B;
+  hipLaunchKernelGGL(k_build_bounds, dim3(1024), dim3(256), 0, s, density, rx, ry, rz, bshift, bnx, bny, bnz,
+                     max_density, bounds);
   return hipGetLastError();
 }
 

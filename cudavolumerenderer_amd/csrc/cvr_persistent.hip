@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256, kWaves) void k_persistent(MediumParams m, Laun
       ++n_tr;
 #endif
       if (state == S_TRACK) {
-        const int r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY]);
+        const int r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
         if (r == 1) state = S_BOUNDARY;
         else if (r == 2) state = (t < is.dist) ? S_COLLIDE : S_BOUNDARY;
       }

@@ -80,6 +80,15 @@ struct MediumParams {
   // uint wrap at -1, far out-of-range taps) use `density`.
   const float4* __restrict__ cells;   // 2 * rx*ry*rz float4, may be null
   const float4* __restrict__ albedo;  // rx*ry*rz float4 (rgb, w=1)
+  // Brick bounds (DESIGN.md §Brick bounds): for each brick of 2^bshift cells
+  // per axis, q = a u8 upper bound of every density the brick's cells can
+  // interpolate, in units of max_density/254 (255 = no bound).  A Woodcock
+  // tentative point whose brick threshold q*bq is below its test draw is a
+  // null collision whatever the exact density is, so the cell is not fetched.
+  // May be null (every point is fetched).
+  const uint8_t* __restrict__ bounds;
+  uint32_t bshift, bnx, bny;  // brick size log2, bricks per x / y row
+  float bq;                   // (1/254)(1 + 2^-16): q -> bound on rho*inv_sigma
   uint32_t rx, ry, rz;
   float fres_x, fres_y, fres_z;  // (float)res
   float gx, gy, gz;  // (float)(res-1): DeviceVolume::volumeToGrid
@@ -148,6 +157,7 @@ enum {
   STAT_ALBEDO,
   STAT_ESCAPED,
   STAT_TRUNCATED,
+  STAT_FETCH,  // density cells actually fetched (the rest were bounded out)
   STAT_COUNT
 };
 
@@ -269,10 +279,30 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 }
 
 // ---------------------------------------------------------- Woodcock ------
+// True when the brick bound proves that the tentative point at AABB-space
+// coordinate `c` is a null collision for test draw `xi`: the exact test is
+// !(fl(fl(scale*rho)*inv_sigma) < xi) with rho = the trilinear density, and
+// rho <= bound*(1 + 6u) (three fma lerps of values <= bound), so
+// fl(fl(scale*rho)*inv_sigma) <= rho/max_density*(1 + 10u) <= q*bq.  Points
+// whose lower corner is outside the grid (quirk Q5 taps, NaN) are never
+// bounded out.
+CVR_DEV bool bound_rejects(const MediumParams& m, V3 c, float xi) {
+  const float fx1 = __builtin_floorf(c.x * m.gx), fy1 = __builtin_floorf(c.y * m.gy),
+              fz1 = __builtin_floorf(c.z * m.gz);
+  if (!(fx1 >= 0.0f && fx1 < m.fres_x && fy1 >= 0.0f && fy1 < m.fres_y && fz1 >= 0.0f && fz1 < m.fres_z))
+    return false;
+  const uint32_t bx = (uint32_t)fx1 >> m.bshift, by = (uint32_t)fy1 >> m.bshift, bz = (uint32_t)fz1 >> m.bshift;
+  const uint32_t q = m.bounds[(__umul24(bz, m.bny) + by) * m.bnx + bx];
+  return (float)q * m.bq < xi;
+}
+
 // One Woodcock step (Utilities.cuh:134-136,148-152).  Returns 0 = keep
 // tracking, 1 = tentative t beyond max_t (no collision), 2 = accepted.
+// The test value is drawn before the density is looked up: the reference
+// draws it right after the lookup, and nothing between consumes the RNG, so
+// the stream is the same.
 CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
-                          uint32_t& n_steps, uint32_t& n_density) {
+                          uint32_t& n_steps, uint32_t& n_density, uint32_t& n_fetch) {
   const float xi = rng_float(rng);
   // == det_logf(det_fmaxf(xi, EPSILON)): xi is never NaN and the clamped
   // argument is a normal float, so the NaN and subnormal paths are dropped.
@@ -280,9 +310,13 @@ CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float&
   ++n_steps;
   if (!(t <= max_t)) return 1;
   const V3 p = mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z));
-  const float rho = m.scale * density_lookup(m, sub3(p, m.shift));
+  const V3 c = sub3(p, m.shift);
   ++n_density;
-  if (!(rho * m.inv_sigma < rng_float(rng))) return 2;
+  const float xi_test = rng_float(rng);
+  if (m.bounds && bound_rejects(m, c, xi_test)) return 0;
+  ++n_fetch;
+  const float rho = m.scale * density_lookup(m, c);
+  if (!(rho * m.inv_sigma < xi_test)) return 2;
   return 0;
 }
 

@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void k_wf_track(MediumParams m, LaunchParams L
     if (!__any(active)) break;
     // ---- one Woodcock step per active lane ---------------------------------
     if (active) {
-      const int r = woodcock_step(m, o, d, max_t, t, rng, c[STAT_STEPS], c[STAT_DENSITY]);
+      const int r = woodcock_step(m, o, d, max_t, t, rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
       if (r != 0) {
         P.t[slot] = t;
         P.r0[slot] = rng.v0;

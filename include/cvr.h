@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CVR_ABI_VERSION 1
+#define CVR_ABI_VERSION 2
 
 enum {
   CVR_OK = 0,
@@ -70,7 +70,9 @@ typedef enum {
                                  in HBM, 2 x 16 B loads per Woodcock step); applies at set_medium */,
   CVR_OPT_WAVES = 10,         /* persistent kernel register budget: 4 (default), 5, 6, 8 waves/SIMD */
   CVR_OPT_ORDER = 11,         /* 1 (default): 8x8-pixel blocks, samples innermost; 0: path-id order */
-  CVR_OPT_QUEUES = 12         /* work bands / queues, one per XCD (default 8) */
+  CVR_OPT_QUEUES = 12,        /* work bands / queues, one per XCD (default 8) */
+  CVR_OPT_BOUNDS = 13         /* brick bounds: log2 brick size 1..5, 0 = off (default 2);
+                                 next cvr_set_medium.  Results are identical either way. */
 } cvr_option;
 
 /* HeterogeneousMedium + GGX boundary (Medium.h:110-190, Bsdf.h:17-30). */
@@ -99,6 +101,7 @@ typedef struct cvr_stats {
   uint64_t iterations; /* wavefront: events/track kernel pairs of the last launch */
   double track_ms;     /* wavefront: summed device time of the tracking kernels (CVR_OPT_TIMING) */
   double events_ms;    /* wavefront: summed device time of the event kernels (CVR_OPT_TIMING) */
+  uint64_t fetches;    /* density cells fetched (evaluations not settled by a brick bound) */
 } cvr_stats;
 
 typedef struct cvr_path_record {

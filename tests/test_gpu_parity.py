@@ -219,3 +219,39 @@ def test_errors_are_reported_not_fatal(cvr, scenes):
     assert "CVR_ERR_STATE" in str(e.value)
     with pytest.raises(cvr.CvrError):
         ctx.set_option(cvr.OPT_EVENT_THRESHOLD, 0)
+
+
+@pytest.mark.parametrize("scene_key", ["manix_small", "hetvol"])
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+def test_brick_bounds_do_not_change_results(cvr, scenes, scene_key, kernel):
+    """Brick bounds (MediumParams::bounds) only skip fetches whose test is
+    decided anyway: per-path records are bit-identical for every brick size
+    and with the bounds off; only the fetch count changes."""
+    scene = scenes[scene_key]
+    W = H = 64
+    iters = 2
+    iv, r2v = cvr.default_camera(W, H)
+    want = None
+    for bshift in [0, 1, 2, 3, 5]:
+        ctx = cvr.Context(0, kernel)
+        ctx.set_option(cvr.OPT_BOUNDS, bshift)
+        ctx.set_medium(scene.medium)
+        ctx.set_camera(iv, r2v, (W, H))
+        ctx.init()
+        ctx.set_resolution(W, H)
+        ctx.set_iterations(iters)
+        rec = ctx.trace_paths(0, W * H * iters)
+        ctx.clear_output()
+        ctx.launch_render()
+        st = ctx.stats()
+        assert st.density == rec["n_density"].sum()
+        if bshift == 0:
+            assert st.fetches == st.density
+            want = rec
+            continue
+        assert st.fetches <= st.density
+        if bshift <= 2:
+            assert st.fetches < st.density
+        for f in ("image_id", "flags", "n_segments", "n_steps", "n_density", "n_albedo"):
+            assert np.array_equal(rec[f], want[f]), (bshift, f)
+        assert np.array_equal(rec["T"].view(np.uint32), want["T"].view(np.uint32)), bshift

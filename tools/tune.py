@@ -18,13 +18,16 @@ import cudavolumerenderer_amd as cvr  # noqa: E402
 
 DEFAULT = [
     "naiveSK:",
+    "regenerationSK:bounds=0",
+    "regenerationSK:bounds=1",
     "regenerationSK:",
-    "regenerationSK:waves=3",
-    "regenerationSK:waves=3,ev=48",
-    "regenerationSK:waves=3,ev=60",
+    "regenerationSK:bounds=3",
+    "regenerationSK:bounds=4",
+    "regenerationSK:cells=0",
+    "regenerationSK:bounds=3,cells=0",
+    "regenerationSK:ev=32",
     "regenerationSK:ev=48",
-    "regenerationSK:chunk=512",
-    "regenerationSK:waves=3,chunk=512",
+    "regenerationSK:ev=62",
 ]
 
 
@@ -53,6 +56,8 @@ def main():
         k, d = parse(v)
         c = cvr.Context(0, k)
         c.set_option(cvr.OPT_CELLS, d.get("cells", 1))
+        if "bounds" in d:
+            c.set_option(cvr.OPT_BOUNDS, d["bounds"])
         c.set_medium(scene.medium)
         c.set_camera(iv, r2v, (W, H))
         if "ev" in d:
@@ -87,16 +92,16 @@ def main():
             wall = (time.perf_counter() - t0) * 1e3
             if r > 0:
                 times[v].append(wall)
-                extra[v] = (st.kernel_ms, st.iterations, st.track_ms, st.events_ms, st.steps, st.escaped)
+                extra[v] = (st.kernel_ms, st.iterations, st.track_ms, st.events_ms, st.steps, st.escaped, st.fetches)
     cu, grid = ctxs[-1][1].device_info()
     print(f"CUs {cu}, persistent grid {grid} blocks; steps/launch {st.steps}, density {st.density}")
     for v, _ in ctxs:
         t = np.array(times[v])
-        kms, its, tms, ems, steps, esc = extra[v]
+        kms, its, tms, ems, steps, esc, fetches = extra[v]
         gsteps = steps / (np.median(t) * 1e-3) / 1e9
         print(f"{v:42s} wall {np.median(t):8.3f} ms (min {t.min():7.3f}) dev {kms:8.3f}  it {its:4d} "
               f"track {tms:7.3f} events {ems:7.3f}  {W * H * a.iters / np.median(t) / 1e3:7.1f} Msamples/s "
-              f"{gsteps:6.2f} Gsteps/s  esc {esc}", flush=True)
+              f"{gsteps:6.2f} Gsteps/s  esc {esc} fetch {fetches / max(st.density, 1):.3f}", flush=True)
 
 
 if __name__ == "__main__":
