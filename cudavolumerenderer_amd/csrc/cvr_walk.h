@@ -279,28 +279,18 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 }
 
 // ---------------------------------------------------------- Woodcock ------
-// True when the brick bound proves that the tentative point at AABB-space
-// coordinate `c` is a null collision for test draw `xi`: the exact test is
-// !(fl(fl(scale*rho)*inv_sigma) < xi) with rho = the trilinear density, and
-// rho <= bound*(1 + 6u) (three fma lerps of values <= bound), so
-// fl(fl(scale*rho)*inv_sigma) <= rho/max_density*(1 + 10u) <= q*bq.  Points
-// whose lower corner is outside the grid (quirk Q5 taps, NaN) are never
-// bounded out.
-CVR_DEV bool bound_rejects(const MediumParams& m, V3 c, float xi) {
-  const float fx1 = __builtin_floorf(c.x * m.gx), fy1 = __builtin_floorf(c.y * m.gy),
-              fz1 = __builtin_floorf(c.z * m.gz);
-  if (!(fx1 >= 0.0f && fx1 < m.fres_x && fy1 >= 0.0f && fy1 < m.fres_y && fz1 >= 0.0f && fz1 < m.fres_z))
-    return false;
-  const uint32_t bx = (uint32_t)fx1 >> m.bshift, by = (uint32_t)fy1 >> m.bshift, bz = (uint32_t)fz1 >> m.bshift;
-  const uint32_t q = m.bounds[(__umul24(bz, m.bny) + by) * m.bnx + bx];
-  return (float)q * m.bq < xi;
-}
-
 // One Woodcock step (Utilities.cuh:134-136,148-152).  Returns 0 = keep
 // tracking, 1 = tentative t beyond max_t (no collision), 2 = accepted.
+//
 // The test value is drawn before the density is looked up: the reference
-// draws it right after the lookup, and nothing between consumes the RNG, so
-// the stream is the same.
+// draws it right after the lookup and nothing in between consumes the RNG,
+// so the stream is the same.  Brick bounds (MediumParams::bounds): the exact
+// test is !(fl(fl(scale*rho)*inv_sigma) < xi) with rho the trilinear density
+// of the cell, and rho <= bound*(1 + 9u) (three fma lerps of values <=
+// bound), so fl(fl(scale*rho)*inv_sigma) <= rho/max_density*(1 + 14u) <=
+// q*bq: when q*bq < xi the point is a null collision whatever rho is, and the
+// cell is not fetched.  Points whose lower corner lies outside the grid
+// (quirk Q5 taps, NaN) use q = 255 (never bounded out) and the 8-tap gather.
 CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
                           uint32_t& n_steps, uint32_t& n_density, uint32_t& n_fetch) {
   const float xi = rng_float(rng);
@@ -309,13 +299,31 @@ CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float&
   t = det_fmaf(-det_logf_normal(xi < CVR_EPSILON_F ? CVR_EPSILON_F : xi), m.inv_sigma, t);
   ++n_steps;
   if (!(t <= max_t)) return 1;
-  const V3 p = mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z));
-  const V3 c = sub3(p, m.shift);
+  const V3 c = sub3(mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z)), m.shift);
   ++n_density;
   const float xi_test = rng_float(rng);
-  if (m.bounds && bound_rejects(m, c, xi_test)) return 0;
+  // cell of the tentative point (DeviceVolume::volumeToGrid + floor)
+  const float cx = c.x * m.gx, cy = c.y * m.gy, cz = c.z * m.gz;
+  const float fx1 = __builtin_floorf(cx), fy1 = __builtin_floorf(cy), fz1 = __builtin_floorf(cz);
+  // bitwise &: one mask, no short-circuit branches; NaN fails every compare
+  const bool in = (fx1 >= 0.0f) & (fx1 < m.fres_x) & (fy1 >= 0.0f) & (fy1 < m.fres_y) & (fz1 >= 0.0f) &
+                  (fz1 < m.fres_z);
+  const uint32_t x1 = in ? (uint32_t)fx1 : 0u, y1 = in ? (uint32_t)fy1 : 0u, z1 = in ? (uint32_t)fz1 : 0u;
+  if (m.bounds) {
+    const uint32_t bi = (__umul24(z1 >> m.bshift, m.bny) + (y1 >> m.bshift)) * m.bnx + (x1 >> m.bshift);
+    const uint32_t q = in ? (uint32_t)m.bounds[bi] : 255u;
+    if ((float)q * m.bq < xi_test) return 0;
+  }
   ++n_fetch;
-  const float rho = m.scale * density_lookup(m, c);
+  float dens;
+  if (in && m.cells) {
+    const uint32_t cell = (__umul24(z1, m.ry) + y1) * m.rx + x1;
+    const float4 lo = m.cells[2 * cell], hi = m.cells[2 * cell + 1];
+    dens = trilerp8(lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, cx - fx1, cy - fy1, cz - fz1);
+  } else {
+    dens = density_lookup_gather(m, c);
+  }
+  const float rho = m.scale * dens;
   if (!(rho * m.inv_sigma < xi_test)) return 2;
   return 0;
 }

@@ -21,7 +21,6 @@ W = H = 1024
 iv, r2v = cvr.default_camera(W, H)
 for ev in (56, 32, 16):
     c = cvr.Context(0, "regenerationSK")
-    c.set_option(cvr.OPT_SCHEDULER, 1)
     c.set_option(cvr.OPT_EVENT_THRESHOLD, ev)
     c.set_medium(scene.medium)
     c.set_camera(iv, r2v, (W, H))
