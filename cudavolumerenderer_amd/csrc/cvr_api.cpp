@@ -88,9 +88,13 @@ struct cvr_ctx {
 
   int cu_count = 0;
   int persistent_grid = 0;
+  int pool_grid = 0;
+  uint32_t pool_tail = 16;
+  int wpool_grid = 0;
+  uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
-  int scheduler = 0;  // 0 single persistent kernel (default), 1 wavefront kernel pair
+  int scheduler = 3;  // 0 persistent, 1 wavefront pair, 2 workgroup pool, 3 wave-private pool (default)
   int waves = 4;      // persistent kernel register budget (waves per SIMD)
 
   // wavefront pool (cvr_wavefront.hip)
@@ -173,6 +177,8 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   L.stats = reinterpret_cast<unsigned long long*>(c->d_work + kWorkStats);
   L.chunk = c->chunk ? c->chunk : 256;
   L.ev_thresh = c->ev_thresh ? c->ev_thresh : 1;
+  L.tail = c->pool_tail;
+  L.batch = c->swap_batch;
   // work order (see LaunchParams): pixel blocks with samples innermost, one
   // contiguous band of blocks per queue, when the launch covers whole samples
   const uint64_t P = L.tile_px;
@@ -210,6 +216,14 @@ int do_init(cvr_ctx* c) {
   HIP_TRY(c, cvr::persistent_occupancy(scatter_eps_for(c), c->waves, &bpc));
   if (bpc < 1) bpc = 1;
   c->persistent_grid = bpc * c->cu_count;
+  int pbpc = 0;
+  HIP_TRY(c, cvr::pool_occupancy(scatter_eps_for(c), &pbpc));
+  if (pbpc < 1) pbpc = 1;
+  c->pool_grid = pbpc * c->cu_count;
+  int wbpc = 0;
+  HIP_TRY(c, cvr::wpool_occupancy(scatter_eps_for(c), &wbpc));
+  if (wbpc < 1) wbpc = 1;
+  c->wpool_grid = wbpc * c->cu_count;
   int tbpc = 0;
   HIP_TRY(c, cvr::wf_track_occupancy(&tbpc));
   if (tbpc < 1) tbpc = 1;
@@ -567,7 +581,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->grid_override = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_SCHEDULER:
-      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "scheduler must be 0 or 1");
+      if (v < 0 || v > 3) return set_err(&c->err, CVR_ERR_INVALID, "scheduler must be 0..3");
       c->scheduler = (int)v;
       return CVR_OK;
     case CVR_OPT_POOL:
@@ -590,6 +604,14 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
         return set_err(&c->err, CVR_ERR_INVALID, "waves must be 3, 4, 5, 6 or 8");
       c->waves = (int)v;
       c->inited = false;
+      return CVR_OK;
+    case CVR_OPT_BATCH:
+      if (v < 1 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "batch must be 1..64");
+      c->swap_batch = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_TAIL:
+      if (v < 0 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "tail must be 0..64");
+      c->pool_tail = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_BOUNDS:
       // takes effect at the next cvr_set_medium
@@ -644,6 +666,12 @@ int cvr_launch_render(cvr_ctx* c) {
   } else if (c->scheduler == 0) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
     HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, c->waves, grid, c->stream));
+  } else if (c->scheduler == 2) {
+    const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->pool_grid;
+    HIP_TRY(c, cvr::launch_pool(c->m, L, eps, grid, c->stream));
+  } else if (c->scheduler == 3) {
+    const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->wpool_grid;
+    HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }

@@ -118,6 +118,8 @@ struct LaunchParams {
   unsigned long long* stats;  // CVR_STAT_* counters (zeroed per launch)
   uint32_t chunk;         // paths per wave dequeue
   uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
+  uint32_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track
+  uint32_t batch;         // wave-pool kernel: idle lanes that trigger a swap
   // Work order (scheduling only; results are bound to path ids).  order 0:
   // path ids in sample-major order from one queue.  order 1: 8x8-pixel
   // blocks with all their samples back to back (path_first must be a

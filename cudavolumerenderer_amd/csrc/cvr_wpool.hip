@@ -1,0 +1,389 @@
+// cvr_wpool.hip - regenerationSK with a wave-private path pool in LDS (gfx950).
+//
+// Semantics: RegenerationVolPTsk_kernel::d_render_single_thread_regeneration
+// (RegenerationVolPTsk_kernel.cuh:146-232): persistent work-items take new
+// paths from a global counter as paths end; no -eps at the scatter point
+// (:212).  The RNG is bound to the path id, so the image is
+// independent of the scheduling below.
+//
+// Why: with brick bounds the walk is VALU-bound, and a
+// wave whose 64 lanes each own one path keeps about half of its lanes idle in
+// the Woodcock loop (a finished segment waits until enough of the wave is
+// done before the event code runs, and that code then runs once per event
+// kind present).  Here each wave (one workgroup = one wave) owns kSlots > 64
+// paths kept in LDS:
+//   * TRACK: lanes run Woodcock steps on track-ready paths; a lane whose
+//     segment ends files it in the boundary or collision list and takes the
+//     next track-ready path, so all 64 lanes keep stepping while the wave has
+//     more paths than lanes.
+//   * EVENT: once 64 events are waiting, the tracking lanes park (t, rng) in
+//     their slots and the wave handles 64 events at once, boundary events
+//     first, then collisions, so each part runs one kind of event code on a
+//     full wave; roulette, regeneration and the AABB test follow, and each
+//     path goes back to the track-ready ring or the boundary list.
+// The pool is private to the wave and the wave runs in lockstep, so the lists
+// need no atomics and no barriers: their counters are wave-uniform scalars.
+#include <hip/hip_runtime.h>
+
+#include "cvr_kernels.h"
+#include "cvr_walk.h"
+
+#ifndef CVR_STAMPS
+#define CVR_STAMPS 0
+#endif
+
+namespace cvr {
+
+namespace {
+
+// Paths per wave (about 2 per lane).  125 keeps pool + launch parameters under
+// 10 KB so 16 single-wave workgroups (4 waves per SIMD) fit a CU's 160 KB LDS.
+constexpr int kSlots = 125;
+
+struct WavePool {
+  float ox[kSlots], oy[kSlots], oz[kSlots], dx[kSlots], dy[kSlots], dz[kSlots];
+  float tx[kSlots], ty[kSlots], tz[kSlots], dist[kSlots], t[kSlots];
+  uint32_t r0[kSlots], r1[kSlots], r2[kSlots], r3[kSlots], r4[kSlots], rd[kSlots];
+  uint32_t img[kSlots];
+  uint32_t meta[kSlots];   // bits 0-2 normal code, bit 3 inside, bits 4.. segments so far
+  uint8_t ready[kSlots];   // ring of track-ready slots
+  uint8_t lb[kSlots];      // stack of boundary events
+  uint8_t lc[kSlots];      // stack of real collisions
+  uint8_t ln[kSlots];      // stack of slots waiting for a new path
+};
+
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t normal_code(V3 n) {
+  return n.x > 0.f ? 1u : n.x < 0.f ? 2u : n.y > 0.f ? 3u : n.y < 0.f ? 4u : n.z > 0.f ? 5u : n.z < 0.f ? 6u : 0u;
+}
+__device__ __forceinline__ V3 normal_of(uint32_t c) {
+  const float s = (c & 1u) ? 1.0f : -1.0f;
+  return c == 0u ? mk3(0, 0, 0) : c <= 2u ? mk3(s, 0, 0) : c <= 4u ? mk3(0, s, 0) : mk3(0, 0, s);
+}
+
+__device__ __forceinline__ void store_full(WavePool& S, uint32_t s, const PathState& ps, const Isect& is,
+                                           uint32_t nseg) {
+  S.ox[s] = ps.o.x;
+  S.oy[s] = ps.o.y;
+  S.oz[s] = ps.o.z;
+  S.dx[s] = ps.d.x;
+  S.dy[s] = ps.d.y;
+  S.dz[s] = ps.d.z;
+  S.tx[s] = ps.T.x;
+  S.ty[s] = ps.T.y;
+  S.tz[s] = ps.T.z;
+  S.dist[s] = is.dist;
+  S.t[s] = 0.0f;
+  S.r0[s] = ps.rng.v0;
+  S.r1[s] = ps.rng.v1;
+  S.r2[s] = ps.rng.v2;
+  S.r3[s] = ps.rng.v3;
+  S.r4[s] = ps.rng.v4;
+  S.rd[s] = ps.rng.d;
+  S.img[s] = ps.image_id;
+  S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
+}
+__device__ __forceinline__ void load_full(const WavePool& S, uint32_t s, PathState& ps, Isect& is, uint32_t& nseg,
+                                          float& t) {
+  ps.o = mk3(S.ox[s], S.oy[s], S.oz[s]);
+  ps.d = mk3(S.dx[s], S.dy[s], S.dz[s]);
+  ps.T = mk3(S.tx[s], S.ty[s], S.tz[s]);
+  is.dist = S.dist[s];
+  t = S.t[s];
+  ps.rng = Rng{S.r0[s], S.r1[s], S.r2[s], S.r3[s], S.r4[s], S.rd[s]};
+  ps.image_id = S.img[s];
+  const uint32_t meta = S.meta[s];
+  is.normal = normal_of(meta & 7u);
+  is.inside = (meta & 8u) != 0u;
+  nseg = meta >> 4;
+}
+__device__ __forceinline__ void store_track(WavePool& S, uint32_t s, float t, const Rng& rng) {
+  S.t[s] = t;
+  S.r0[s] = rng.v0;
+  S.r1[s] = rng.v1;
+  S.r2[s] = rng.v2;
+  S.r3[s] = rng.v3;
+  S.r4[s] = rng.v4;
+  S.rd[s] = rng.d;
+}
+
+enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
+
+// The wave's path cursor into the global work queues (as k_persistent).
+struct Cursor {
+  uint32_t next, end, q, home;
+  bool exhausted;
+};
+
+}  // namespace
+
+template <bool kScatterEps>
+__global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk) {
+  __shared__ WavePool S;
+  // The launch parameters live in LDS: only the event code reads them, and
+  // keeping them in SGPRs for the whole kernel spills the step loop's
+  // scalars (v_readlane reloads in every Woodcock step).
+  __shared__ LaunchParams L;
+  const uint32_t lane = threadIdx.x;
+  if (lane == 0) L = Lk;
+  __syncthreads();
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t seg_sum = 0;
+  Cursor cur{0, 0, 0, (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % L.n_queues, false};
+  const uint32_t batch = L.batch;  // TRACK: swap finished segments once this many lanes are idle
+  // wave-uniform list state
+  uint32_t ready_head = 0, n_ready = 0, n_lb = 0, n_lc = 0;
+  uint32_t n_ln = kSlots;  // slots waiting for a new path (all of them at the start)
+  for (uint32_t i = lane; i < (uint32_t)kSlots; i += 64u) S.ln[i] = (uint8_t)i;
+#if CVR_STAMPS
+  // event cycles, track cycles, event batches, track iterations, event-code cycles, regen+AABB cycles
+  unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long t_mark = __builtin_amdgcn_s_memtime();
+#endif
+
+#if CVR_STAMPS
+  unsigned long long t_regen = 0;
+#endif
+  for (;;) {
+    // ================================================= TRACK ==============
+    // The track state is fresh per outer iteration and parked in the pool
+    // before the event code runs, so nothing of it is live across that code
+    // (keeps the step loop free of spills).
+    int slot = -1;      // pool slot of the lane's path, -1 = none
+    bool fin = false;   // the segment ended; filed at the next swap
+    bool coll = false;  // ... as a real collision (else a boundary)
+    V3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
+    Rng rng{0, 0, 0, 0, 0, 0};
+    float t = 0.0f, max_t = 0.0f;
+    for (;;) {
+      const unsigned long long trk = __ballot(slot >= 0 && !fin);
+      const uint32_t n_trk = (uint32_t)__popcll(trk);
+      // ---- swap: file finished segments, pull track-ready paths ----------
+      if (64u - n_trk >= batch || n_trk == 0u) {
+        if (fin) store_track(S, (uint32_t)slot, t, rng);
+        const unsigned long long mc = __ballot(fin && coll), mb = __ballot(fin && !coll);
+        if (fin && coll) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
+        if (fin && !coll) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
+        n_lc += (uint32_t)__popcll(mc);
+        n_lb += (uint32_t)__popcll(mb);
+        if (fin) {
+          slot = -1;
+          fin = false;
+        }
+        const unsigned long long idle = __ballot(slot < 0);
+        const uint32_t k = min((uint32_t)__popcll(idle), n_ready), rank = lane_rank(idle);
+        if (slot < 0 && rank < k) {
+          const uint32_t r = ready_head + rank;
+          const uint32_t s = S.ready[r >= (uint32_t)kSlots ? r - kSlots : r];
+          slot = (int)s;
+          o = mk3(S.ox[s], S.oy[s], S.oz[s]);
+          d = mk3(S.dx[s], S.dy[s], S.dz[s]);
+          rng = Rng{S.r0[s], S.r1[s], S.r2[s], S.r3[s], S.r4[s], S.rd[s]};
+          t = S.t[s];
+          max_t = S.dist[s];
+        }
+        ready_head += k;
+        if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
+        n_ready -= k;
+      }
+      const uint32_t n_act = (uint32_t)__popcll(__ballot(slot >= 0 && !fin));
+      const uint32_t n_fin = (uint32_t)__popcll(__ballot(fin));
+      // EVENT next: a full wave of waiting events, slots never filled, or
+      // nothing left to track.  Park: tracking lanes return (t, rng) to the
+      // pool, finished lanes are filed.
+      if (n_lb + n_lc + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
+        if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
+        const unsigned long long mr = __ballot(slot >= 0 && !fin);
+        const unsigned long long mc = __ballot(fin && coll), mb = __ballot(fin && !coll);
+        if (slot >= 0 && !fin) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)slot;
+        if (fin && coll) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
+        if (fin && !coll) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
+        n_ready += (uint32_t)__popcll(mr);
+        n_lc += (uint32_t)__popcll(mc);
+        n_lb += (uint32_t)__popcll(mb);
+        break;
+      }
+      // ---- one Woodcock step (Utilities.cuh:147-152) ---------------------
+#if CVR_STAMPS
+      ++st[3];
+#endif
+      if (slot >= 0 && !fin) {
+        const int r = woodcock_step(m, o, d, max_t, t, rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
+        if (r != 0) {
+          fin = true;
+          coll = (r == 2) && (t < max_t);
+        }
+      }
+    }
+#if CVR_STAMPS
+    {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      st[1] += now - t_mark;
+      t_mark = now;
+      ++st[2];
+    }
+#endif
+    // no path left (new-path slots only count while the queues have paths)
+    if (n_lb + n_lc == 0u && n_ready == 0u && (n_ln == 0u || cur.exhausted)) break;
+
+    // ================================================= EVENT ==============
+    // One batch of up to 64 items, [boundary | collision | new] so each part
+    // runs one kind of code on consecutive lanes.  No item loops: a path
+    // that dies (roulette, escape, truncation) files its slot in the new
+    // list and is regenerated by a later batch.
+    {
+      const uint32_t tb = min(n_lb, 64u), tc = min(n_lc, 64u - tb), tn = min(n_ln, 64u - tb - tc);
+      uint32_t kind = K_NONE, s = 0;
+      if (lane < tb) {
+        kind = K_BOUNDARY;
+        s = S.lb[n_lb - 1u - lane];
+      } else if (lane < tb + tc) {
+        kind = K_COLLIDE;
+        s = S.lc[n_lc - 1u - (lane - tb)];
+      } else if (lane < tb + tc + tn) {
+        kind = K_NEW;
+        s = S.ln[n_ln - 1u - (lane - tb - tc)];
+      }
+      n_lb -= tb;
+      n_lc -= tc;
+      n_ln -= tn;
+      PathState ps;
+      Isect is;
+      uint32_t nseg = 0;
+      float t_hit = 0.0f;
+      bool alive = false;
+      if (kind <= K_COLLIDE) load_full(S, s, ps, is, nseg, t_hit);
+      if (kind == K_BOUNDARY) {
+        boundary_event(m, ps, is);
+        alive = roulette(ps);
+      } else if (kind == K_COLLIDE) {
+        scatter_event<kScatterEps>(m, ps, t_hit);
+        ++c[STAT_ALBEDO];
+        alive = roulette(ps);
+      }
+      if (kind <= K_COLLIDE && !alive) seg_sum += nseg;
+      // ---- regeneration (new items): the wave's cursor into the global queues
+      const unsigned long long want = __ballot(kind == K_NEW);
+      if (want != 0ull) {
+        const uint32_t rank = lane_rank(want);
+        uint32_t given = 0;  // new items [0, given) get a path
+        while (given < (uint32_t)__popcll(want) && !cur.exhausted) {
+          if (cur.next == cur.end) {
+            uint32_t b = 0xFFFFFFFFu, qsel = 0;
+            if (lane == 0) {
+              for (uint32_t k = 0; k < L.n_queues; ++k) {
+                const uint32_t q = (cur.home + k) % L.n_queues;
+                const uint32_t got = atomicAdd(L.queue + 16 * q, L.chunk);
+                if (got < queue_units(L, q)) {
+                  b = got;
+                  qsel = q;
+                  break;
+                }
+              }
+            }
+            b = __shfl(b, 0);
+            qsel = __shfl(qsel, 0);
+            if (b == 0xFFFFFFFFu) {
+              cur.exhausted = true;
+              break;
+            }
+            cur.q = cur.home = qsel;
+            cur.next = b;
+            cur.end = min(b + L.chunk, queue_units(L, qsel));
+          }
+          const uint32_t take = min((uint32_t)__popcll(want) - given, cur.end - cur.next);
+          if (kind == K_NEW && rank >= given && rank < given + take) {
+            path_begin(L, unit_to_path(L, cur.q, cur.next + (rank - given)), ps);
+            is.normal = mk3(0, 0, 0);
+            nseg = 0;
+            alive = true;
+            ++c[STAT_PATHS];
+          }
+          cur.next += take;
+          given += take;
+        }
+      }
+      // ---- next segment: AABB test (NaiveVolPTsk_kernel.cuh:33-47) -------
+      bool to_ready = false, to_lb = false, to_ln = false;
+      if (alive) {
+        if (L.max_segments && nseg >= L.max_segments) {
+          ++c[STAT_TRUNCATED];
+          seg_sum += nseg;
+          to_ln = true;
+        } else {
+          ++nseg;
+          if (!aabb_intersect(m, ps.o, ps.d, is)) {
+            splat(L, ps);
+            ++c[STAT_ESCAPED];
+            seg_sum += nseg;
+            to_ln = true;
+          } else {
+            store_full(S, s, ps, is, nseg);
+            to_ready = is.inside;  // medium: Woodcock from t = 0
+            to_lb = !is.inside;    // no medium: boundary at isect.dist
+          }
+        }
+      } else if (kind <= K_COLLIDE) {
+        to_ln = true;  // the path died in roulette
+      }
+      // a new item that got no path (queues exhausted) leaves its slot empty
+#if CVR_STAMPS
+      t_regen = __builtin_amdgcn_s_memtime();
+#endif
+      const unsigned long long mr = __ballot(to_ready), mb = __ballot(to_lb), mn = __ballot(to_ln);
+      if (to_ready) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)s;
+      if (to_lb) S.lb[n_lb + lane_rank(mb)] = (uint8_t)s;
+      if (to_ln) S.ln[n_ln + lane_rank(mn)] = (uint8_t)s;
+      n_ready += (uint32_t)__popcll(mr);
+      n_lb += (uint32_t)__popcll(mb);
+      n_ln += (uint32_t)__popcll(mn);
+    }
+#if CVR_STAMPS
+    {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      st[0] += now - t_mark;
+      st[5] += t_regen - t_mark;
+      t_mark = now;
+    }
+#endif
+  }
+
+  // ---- counters ------------------------------------------------------------
+  c[STAT_SEGMENTS] = seg_sum;
+#pragma unroll
+  for (int k = 0; k < STAT_COUNT; ++k) {
+    unsigned long long v = c[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (lane == 0 && v) atomicAdd(L.stats + k, v);
+  }
+#if CVR_STAMPS
+  {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    st[1] += now - t_mark;
+  }
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) atomicAdd(L.stats + 16 + k, st[k]);
+#endif
+}
+
+hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
+                        hipStream_t s) {
+  if (L.path_count == 0) return hipSuccess;
+  if (scatter_eps)
+    hipLaunchKernelGGL(k_wpool<true>, dim3(grid), dim3(64), 0, s, m, L);
+  else
+    hipLaunchKernelGGL(k_wpool<false>, dim3(grid), dim3(64), 0, s, m, L);
+  return hipGetLastError();
+}
+
+hipError_t wpool_occupancy(bool scatter_eps, int* blocks_per_cu) {
+  const void* fn = scatter_eps ? reinterpret_cast<const void*>(&k_wpool<true>)
+                               : reinterpret_cast<const void*>(&k_wpool<false>);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, 0);
+}
+
+}  // namespace cvr

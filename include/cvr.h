@@ -63,7 +63,8 @@ typedef enum {
   CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
   CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
   CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
-  CVR_OPT_SCHEDULER = 6,      /* regenerationSK: 0 single persistent kernel (default), 1 wavefront pair */
+  CVR_OPT_SCHEDULER = 6,      /* regenerationSK: 0 single persistent kernel, 1 wavefront pair,
+                                 2 workgroup path pool in LDS, 3 wave-private path pool in LDS (default) */
   CVR_OPT_POOL = 7,           /* wavefront ray-slot pool size (default 2^21) */
   CVR_OPT_TIMING = 8,         /* 1: time every wavefront kernel (track_ms / events_ms) */
   CVR_OPT_CELLS = 9           /* 1 (default): corner-replicated density cells (8x density bytes
@@ -71,8 +72,10 @@ typedef enum {
   CVR_OPT_WAVES = 10,         /* persistent kernel register budget: 4 (default), 5, 6, 8 waves/SIMD */
   CVR_OPT_ORDER = 11,         /* 1 (default): 8x8-pixel blocks, samples innermost; 0: path-id order */
   CVR_OPT_QUEUES = 12,        /* work bands / queues, one per XCD (default 8) */
-  CVR_OPT_BOUNDS = 13         /* brick bounds: log2 brick size 1..5, 0 = off (default 2);
+  CVR_OPT_BOUNDS = 13,        /* brick bounds: log2 brick size 1..5, 0 = off (default 2);
                                  next cvr_set_medium.  Results are identical either way. */
+  CVR_OPT_TAIL = 14,          /* pool scheduler: lanes below which a wave ends a track phase (16) */
+  CVR_OPT_BATCH = 15          /* wave-pool scheduler: idle lanes that trigger a refill (8) */
 } cvr_option;
 
 /* HeterogeneousMedium + GGX boundary (Medium.h:110-190, Bsdf.h:17-30). */

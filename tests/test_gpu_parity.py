@@ -255,3 +255,52 @@ def test_brick_bounds_do_not_change_results(cvr, scenes, scene_key, kernel):
         for f in ("image_id", "flags", "n_segments", "n_steps", "n_density", "n_albedo"):
             assert np.array_equal(rec[f], want[f]), (bshift, f)
         assert np.array_equal(rec["T"].view(np.uint32), want["T"].view(np.uint32)), bshift
+
+
+@pytest.mark.parametrize("scene_key", ["manix_small", "hetvol", "bucky"])
+def test_pool_scheduler_matches_persistent(cvr, scenes, scene_key):
+    """Scheduler 2 (workgroup path pool in LDS) renders exactly the paths of
+    the persistent kernel: same counters, same pixels up to fp32 atomic
+    order, for several tails, grids and chunk sizes."""
+    scene = scenes[scene_key]
+    W = H = 128
+    ref, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+    ref.set_option(cvr.OPT_SCHEDULER, 0)  # the per-wave persistent kernel
+    img0, st0 = ref.render_image(W, H, (1, 1), 4)
+    key0 = (st0.paths, st0.segments, st0.steps, st0.density, st0.albedo, st0.escaped, st0.fetches)
+    for tail, grid, chunk, order in [(16, 0, 256, 1), (0, 0, 64, 1), (48, 5, 256, 1), (64, 1, 7, 0),
+                                     (16, 3, 1, 1)]:
+        ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+        ctx.set_option(cvr.OPT_SCHEDULER, 2)
+        ctx.set_option(cvr.OPT_TAIL, tail)
+        ctx.set_option(cvr.OPT_GRID, grid)
+        ctx.set_option(cvr.OPT_CHUNK, chunk)
+        ctx.set_option(cvr.OPT_ORDER, order)
+        img, st = ctx.render_image(W, H, (1, 1), 4)
+        key = (st.paths, st.segments, st.steps, st.density, st.albedo, st.escaped, st.fetches)
+        assert key == key0, (tail, grid, chunk, order)
+        assert_pixels_close(img, img0, 4)
+
+
+@pytest.mark.parametrize("scene_key", ["manix_small", "hetvol", "bucky"])
+def test_wave_pool_scheduler_matches_persistent(cvr, scenes, scene_key):
+    """Scheduler 3 (wave-private path pool in LDS) renders exactly the paths
+    of the persistent kernel for several swap batches, grids and chunks."""
+    scene = scenes[scene_key]
+    W = H = 128
+    ref, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+    ref.set_option(cvr.OPT_SCHEDULER, 0)  # the per-wave persistent kernel
+    img0, st0 = ref.render_image(W, H, (1, 1), 4)
+    key0 = (st0.paths, st0.segments, st0.steps, st0.density, st0.albedo, st0.escaped, st0.fetches)
+    for batch, grid, chunk, order in [(8, 0, 256, 1), (1, 0, 64, 1), (64, 5, 256, 1), (16, 1, 7, 0),
+                                      (32, 3, 1, 1)]:
+        ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+        ctx.set_option(cvr.OPT_SCHEDULER, 3)
+        ctx.set_option(cvr.OPT_BATCH, batch)
+        ctx.set_option(cvr.OPT_GRID, grid)
+        ctx.set_option(cvr.OPT_CHUNK, chunk)
+        ctx.set_option(cvr.OPT_ORDER, order)
+        img, st = ctx.render_image(W, H, (1, 1), 4)
+        key = (st.paths, st.segments, st.steps, st.density, st.albedo, st.escaped, st.fetches)
+        assert key == key0, (batch, grid, chunk, order)
+        assert_pixels_close(img, img0, 4)

@@ -23,7 +23,7 @@ def per_dispatch(d, counter, kname):
 
 def main():
     fdir, wdir, key = sys.argv[1:4]
-    kname = sys.argv[4] if len(sys.argv) > 4 else "k_persistent"
+    kname = sys.argv[4] if len(sys.argv) > 4 else "k_wpool"
     fetch = per_dispatch(fdir, "FETCH_SIZE", kname)
     write = per_dispatch(wdir, "WRITE_SIZE", kname)
     # drop the first (cold) dispatch when there are several

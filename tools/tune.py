@@ -28,6 +28,9 @@ DEFAULT = [
     "regenerationSK:ev=32",
     "regenerationSK:ev=48",
     "regenerationSK:ev=62",
+    "regenerationSK:sched=2",
+    "regenerationSK:sched=2,tail=8",
+    "regenerationSK:sched=2,tail=32",
 ]
 
 
@@ -74,6 +77,10 @@ def main():
             c.set_option(cvr.OPT_QUEUES, d["queues"])
         if "waves" in d:
             c.set_option(cvr.OPT_WAVES, d["waves"])
+        if "batch" in d:
+            c.set_option(cvr.OPT_BATCH, d["batch"])
+        if "tail" in d:
+            c.set_option(cvr.OPT_TAIL, d["tail"])
         if "pool" in d:
             c.set_option(cvr.OPT_POOL, d["pool"])
         c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
