@@ -94,7 +94,7 @@ struct cvr_ctx {
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
-  int scheduler = 3;  // 0 persistent, 1 wavefront pair, 2 workgroup pool, 3 wave-private pool (default)
+  int scheduler = -1;  // 0 persistent, 1 wavefront pair, 2 workgroup pool, 3 wave-private pool, -1 per kernel id
   int waves = 4;      // persistent kernel register budget (waves per SIMD)
 
   // wavefront pool (cvr_wavefront.hip)
@@ -126,7 +126,22 @@ constexpr size_t kWorkQueues = 0, kWorkStats = 512, kWorkDebug = 640, kWorkBytes
 
 namespace {
 
-bool kernel_supported(int k) { return k == CVR_KERNEL_NAIVE_SK || k == CVR_KERNEL_REGENERATION_SK; }
+bool kernel_supported(int k) { return k != CVR_KERNEL_NAIVE_MK && k >= 0 && k < CVR_KERNEL_UNKNOWN; }
+
+// Scheduler that implements each persistent kernel id (results
+// depend only on the kernel id's scatter offset and per-tile seed, quirks
+// Q2/Q6): regenerationSK and sortingSK run the wave-private LDS pool (sorting
+// = event batches sorted by kind), streamingSK the workgroup LDS pool with
+// bulk compaction phases (StreamingVolPTsk's block streaming), streamingMK
+// the multi-kernel wavefront pair (StreamingVolPTmk's device-wide compaction).
+int scheduler_for(const cvr_ctx* c) {
+  if (c->scheduler >= 0) return c->scheduler;
+  switch (c->kernel) {
+    case CVR_KERNEL_STREAMING_SK: return 2;
+    case CVR_KERNEL_STREAMING_MK: return 1;
+    default: return 3;
+  }
+}
 
 // Scatter origin offset per scheduler: every kernel subtracts
 // d*eps at a real collision except single-thread regeneration
@@ -663,13 +678,13 @@ int cvr_launch_render(cvr_ctx* c) {
   c->last_track_ms = c->last_events_ms = 0;
   if (c->kernel == CVR_KERNEL_NAIVE_SK) {
     HIP_TRY(c, cvr::launch_naive(c->m, L, eps, c->stream));
-  } else if (c->scheduler == 0) {
+  } else if (scheduler_for(c) == 0) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
     HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, c->waves, grid, c->stream));
-  } else if (c->scheduler == 2) {
+  } else if (scheduler_for(c) == 2) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->pool_grid;
     HIP_TRY(c, cvr::launch_pool(c->m, L, eps, grid, c->stream));
-  } else if (c->scheduler == 3) {
+  } else if (scheduler_for(c) == 3) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->wpool_grid;
     HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, grid, c->stream));
   } else if (L.path_count > 0) {
@@ -689,9 +704,14 @@ int cvr_synchronize(cvr_ctx* c) {
 int cvr_reset(cvr_ctx* c) {
   if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  // RegenerationVolPTsk::reset: head = 0 (our head is re-zeroed per launch),
-  // seed_ += n_paths.  NaiveVolPTsk::reset only synchronises.
-  if (c->kernel == CVR_KERNEL_REGENERATION_SK) c->seed += (uint32_t)c->n_paths;
+  // Per-tile seed advance (RenderKernelLauncher.cu): RegenerationVolPTsk and
+  // StreamingVolPTmk add n_paths (:359, :480), StreamingVolPTsk and
+  // SortingVolPTsk add 1 (:573, :664), NaiveVolPTsk only synchronises.
+  // Queue heads are re-zeroed per launch.
+  if (c->kernel == CVR_KERNEL_REGENERATION_SK || c->kernel == CVR_KERNEL_STREAMING_MK)
+    c->seed += (uint32_t)c->n_paths;
+  else if (c->kernel == CVR_KERNEL_STREAMING_SK || c->kernel == CVR_KERNEL_SORTING_SK)
+    c->seed += 1u;
   return CVR_OK;
 }
 

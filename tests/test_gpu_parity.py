@@ -40,7 +40,8 @@ def oracle_image(oracle_mod, orc, iv, r2v, W, H, tiles, iters, kernel, seed=0):
     stats = {}
     for k in range(tiles[0] * tiles[1]):
         ox, oy = tw * (k % tiles[0]), th * int(np.float32(k) / np.float32(tiles[0]))
-        sb = (seed + k * n_paths) & 0xFFFFFFFF if kernel == 2 else seed
+        # per-tile seed advance of each launcher's reset() (RenderKernelLauncher.cu:359,480,573,664)
+        sb = {2: seed + k * n_paths, 3: seed + k * n_paths, 4: seed + k, 5: seed + k}.get(kernel, seed) & 0xFFFFFFFF
         L = orc.launch(iv, r2v, (W, H), (tw, th), (ox, oy), kernel, sb)
         tile, st = orc.render(L, 0, n_paths, nthreads=NTHREADS)
         img[oy:oy + th, ox:ox + tw] = tile / np.float32(iters)
@@ -76,7 +77,7 @@ def scenes(cvr):
 
 
 @pytest.mark.parametrize("scene_key", list(SCENES))
-@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK"])
 @pytest.mark.parametrize("cells", [1, 0])
 def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel, cells):
     scene = scenes[scene_key]
@@ -99,7 +100,7 @@ def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel, cells):
     assert c["n_density"].sum() > 0 and (c["flags"] & 1).any()
 
 
-@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK", "sortingSK", "streamingMK"])
 @pytest.mark.parametrize("tiles", [(1, 1), (4, 2), (3, 3)])
 def test_render_image_matches_oracle(cvr, oracle_mod, scenes, kernel, tiles):
     scene = scenes["bucky"]
