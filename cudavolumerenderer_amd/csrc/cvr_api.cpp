@@ -126,7 +126,7 @@ constexpr size_t kWorkQueues = 0, kWorkStats = 512, kWorkDebug = 640, kWorkBytes
 
 namespace {
 
-bool kernel_supported(int k) { return k != CVR_KERNEL_NAIVE_MK && k >= 0 && k < CVR_KERNEL_UNKNOWN; }
+bool kernel_supported(int k) { return k >= 0 && k < CVR_KERNEL_UNKNOWN; }
 
 // Scheduler that implements each persistent kernel id (results
 // depend only on the kernel id's scatter offset and per-tile seed, quirks
@@ -194,6 +194,7 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   L.ev_thresh = c->ev_thresh ? c->ev_thresh : 1;
   L.tail = c->pool_tail;
   L.batch = c->swap_batch;
+  L.naive_mk = c->kernel == CVR_KERNEL_NAIVE_MK ? 1u : 0u;
   // work order (see LaunchParams): pixel blocks with samples innermost, one
   // contiguous band of blocks per queue, when the launch covers whole samples
   const uint64_t P = L.tile_px;
@@ -678,6 +679,8 @@ int cvr_launch_render(cvr_ctx* c) {
   c->last_track_ms = c->last_events_ms = 0;
   if (c->kernel == CVR_KERNEL_NAIVE_SK) {
     HIP_TRY(c, cvr::launch_naive(c->m, L, eps, c->stream));
+  } else if (c->kernel == CVR_KERNEL_NAIVE_MK) {
+    HIP_TRY(c, cvr::launch_naive_mk(c->m, L, c->stream));
   } else if (scheduler_for(c) == 0) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
     HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, c->waves, grid, c->stream));

@@ -70,11 +70,54 @@ __global__ __launch_bounds__(256) void k_naive(MediumParams m, LaunchParams L) {
   flush_stats(L, c);
 }
 
+// ------------------------------------------------------------- naiveMK ----
+// One work-item per (iteration, pixel) path; walk_mk restates the reference's
+// init + extend kernels for one path (cvr_walk.h).
+__global__ __launch_bounds__(256) void k_naive_mk(MediumParams m, LaunchParams L) {
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (tid < L.path_count) {
+    const uint32_t pid = L.path_first + tid;
+    const MkResult r = walk_mk(m, L, pid);
+    c[STAT_PATHS] = 1;
+    c[STAT_SEGMENTS] = r.n_segments;
+    c[STAT_STEPS] = r.n_steps;
+    c[STAT_DENSITY] = r.n_density;
+    c[STAT_FETCH] = r.n_fetch;
+    c[STAT_ALBEDO] = r.n_albedo;
+    c[STAT_TRUNCATED] = (r.flags >> 1) & 1u;
+    if (r.flags & 1u) {
+      PathState ps;
+      ps.image_id = pid % L.tile_px;
+      ps.T = r.T;
+      splat(L, ps);
+      c[STAT_ESCAPED] = 1;
+    }
+  }
+  flush_stats(L, c);
+}
+
 // --------------------------------------------------------------- trace ----
 template <bool kScatterEps>
 __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, PathRecord* rec) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= L.path_count) return;
+  if (L.naive_mk) {
+    const MkResult mr = walk_mk(m, L, L.path_first + tid);
+    PathRecord r = {};
+    r.image_id = (L.path_first + tid) % L.tile_px;
+    r.flags = mr.flags;
+    r.T[0] = mr.T.x;
+    r.T[1] = mr.T.y;
+    r.T[2] = mr.T.z;
+    r.n_segments = mr.n_segments;
+    r.n_steps = mr.n_steps;
+    r.n_density = mr.n_density;
+    r.n_albedo = mr.n_albedo;
+    rec[tid] = r;
+    if (mr.n_fetch) atomicAdd(L.stats + STAT_FETCH, (unsigned long long)mr.n_fetch);
+    return;
+  }
   PathState ps;
   path_begin(L, L.path_first + tid, ps);
   Isect is;
@@ -185,6 +228,12 @@ hipError_t launch_naive(const MediumParams& m, const LaunchParams& L, bool scatt
     hipLaunchKernelGGL(k_naive<true>, dim3(grid), dim3(256), 0, s, m, L);
   else
     hipLaunchKernelGGL(k_naive<false>, dim3(grid), dim3(256), 0, s, m, L);
+  return hipGetLastError();
+}
+
+hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s) {
+  if (L.path_count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_naive_mk, dim3((L.path_count + 255u) / 256u), dim3(256), 0, s, m, L);
   return hipGetLastError();
 }
 

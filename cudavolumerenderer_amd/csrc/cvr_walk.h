@@ -120,6 +120,7 @@ struct LaunchParams {
   uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
   uint32_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track
   uint32_t batch;         // wave-pool kernel: idle lanes that trigger a swap
+  uint32_t naive_mk;      // trace kernel: naiveMK paths (walk_mk) instead of path_begin + loop
   // Work order (scheduling only; results are bound to path ids).  order 0:
   // path ids in sample-major order from one queue.  order 1: 8x8-pixel
   // blocks with all their samples back to back (path_first must be a
@@ -568,6 +569,121 @@ CVR_DEV void splat(const LaunchParams& L, const PathState& ps) {
   atomicAdd(px + 1, ps.T.y);
   atomicAdd(px + 2, ps.T.z);
   px[3] = 1.0f;
+}
+
+// ------------------------------------------------------------ naiveMK -----
+// utilhash / makeSeededRng (Utilities.cuh:157-178): naiveMK re-seeds the RNG
+// from (iteration, pixel, depth) at every kernel launch.
+CVR_DEV uint32_t utilhash(uint32_t a) {
+  a = (a + 0x7ed55d16u) + (a << 12);
+  a = (a ^ 0xc761c23cu) ^ (a >> 19);
+  a = (a + 0x165667b1u) + (a << 5);
+  a = (a + 0xd3a2646cu) ^ (a << 9);
+  a = (a + 0xfd7046c5u) + (a << 3);
+  a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+  return a;
+}
+CVR_DEV void rng_seeded(Rng& s, uint32_t iteration, uint32_t index, uint32_t depth) {
+  rng_init(s, (int32_t)(utilhash(0x80000000u | (depth << 22) | iteration) ^ utilhash(index)));
+}
+
+// Outcome of one naiveMK path (flags as PathRecord: bit0 contributed T,
+// bit1 truncated, bit2 missed the box at init (T = 1), bit3 dropped by a
+// failed GGX sample at init).
+struct MkResult {
+  uint32_t flags;
+  V3 T;
+  uint32_t n_segments, n_steps, n_density, n_fetch, n_albedo;
+};
+
+// NaiveVolPTmk_kernel::d_init + the d_extend bounce loop (NaiveVolPTmk_kernel.cuh:20-151,
+// RenderKernelLauncher.cu:183-272) for path id = iteration * tile_px + pixel.
+// Per path the multi-kernel wavefront reduces to this loop: every live path
+// is extended once per launch, and compaction keeps every live path (quirk
+// Q11 fixed).  Same operation order as the oracle's trace_path_mk.
+CVR_DEV MkResult walk_mk(const MediumParams& m, const LaunchParams& L, uint32_t path_id) {
+  MkResult r{0u, mk3(1.0f, 1.0f, 1.0f), 1u, 0u, 0u, 0u, 0u};
+  const uint32_t image_id = path_id % L.tile_px, iteration = path_id / L.tile_px;
+  PathState ps;
+  ps.image_id = image_id;
+  rng_seeded(ps.rng, iteration, image_id, 0u);
+  {
+    // camera ray as path_begin, on the (iteration, pixel, 0) stream
+    const float px = (float)(image_id % L.tile_w) + (float)L.off[0];
+    const float py = det_floorf((float)image_id / L.tile_res[0]) + (float)L.off[1];
+    const float r0 = rng_float(ps.rng);
+    const float r1 = rng_float(ps.rng);
+    float rx = ((px + r0) * 2.0f) / L.full_res[0] - 1.0f;
+    float ry = ((py + r1) * 2.0f) / L.full_res[1] - 1.0f;
+    rx = L.r2v[0] * rx;
+    ry = L.r2v[1] * ry;
+    const float* M = L.M;
+    ps.o = mk3(0.0f * M[0] + 0.0f * M[1] + 0.0f * M[2] + 1.0f * M[3],
+               0.0f * M[4] + 0.0f * M[5] + 0.0f * M[6] + 1.0f * M[7],
+               0.0f * M[8] + 0.0f * M[9] + 0.0f * M[10] + 1.0f * M[11]);
+    const V3 v = normalize3(mk3(rx, ry, 1.0f));
+    ps.d = mk3(dot3(v, mk3(M[0], M[1], M[2])), dot3(v, mk3(M[4], M[5], M[6])), dot3(v, mk3(M[8], M[9], M[10])));
+  }
+  ps.T = mk3(1.0f, 1.0f, 1.0f);
+  Isect is;
+  is.dist = 0.0f;
+  is.normal = mk3(0, 0, 0);
+  is.inside = false;
+  if (!aabb_intersect(m, ps.o, ps.d, is)) {
+    r.flags = 1u | 4u;
+    return r;
+  }
+  if (is.dist < 0.0f) is.dist = 0.0f;  // clamp to near plane
+  ps.o = add3(ps.o, scl3(ps.d, is.dist));
+  {
+    const Frame fr = frame_from_z(is.normal);
+    const V3 dir = frame_to_local(fr, normalize3(neg3(ps.d)));
+    float weight = 1.0f;
+    if (!ggx_sample(m, dir, ps.rng, ps.d, weight)) {
+      r.flags = 8u;  // dropped: no contribution, T recorded as 0 (as the oracle)
+      r.T = mk3(0.0f, 0.0f, 0.0f);
+      return r;
+    }
+    ps.T = scl3(ps.T, weight);
+    ps.d = frame_to_world(fr, ps.d);
+    ps.o = add3(ps.o, scl3(ps.d, CVR_EPSILON_F));
+  }
+  for (uint32_t depth = 0;; ++depth) {
+    if (L.max_segments && r.n_segments >= L.max_segments) {
+      r.flags |= 2u;
+      break;
+    }
+    ++r.n_segments;
+    rng_seeded(ps.rng, iteration, image_id, depth);
+    (void)rng_float(ps.rng);  // float3 e = rng.getFloat3(), unused (Q12)
+    (void)rng_float(ps.rng);
+    (void)rng_float(ps.rng);
+    is.dist = 0.0f;  // a fresh SimpleIsect per d_extend
+    is.normal = mk3(0, 0, 0);
+    is.inside = false;
+    if (!aabb_intersect(m, ps.o, ps.d, is)) {
+      r.flags |= 1u;
+      break;
+    }
+    float t = 0.0f;
+    bool collided = false;
+    if (is.inside) {
+      int s;
+      do {
+        s = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, r.n_steps, r.n_density, r.n_fetch);
+      } while (s == 0);
+      collided = t < is.dist;
+    }
+    if (!collided) {
+      boundary_event(m, ps, is);
+    } else {
+      scatter_event<true>(m, ps, t);
+      ++r.n_albedo;
+    }
+    if (!roulette(ps)) break;
+  }
+  r.T = ps.T;
+  return r;
 }
 
 }  // namespace cvr

@@ -403,12 +403,131 @@ static void camera_ray(const oracle_launch* L, float px, float py, xorwow_t* rng
            dot3(v, mk3(M[8], M[9], M[10])));
 }
 
+/* ------------------------------------------------------------ naiveMK -- */
+/* utilhash / makeSeededRng (Utilities.cuh:157-178): the naiveMK RNG is
+ * re-seeded from (iteration, pixel, depth) at every kernel launch. */
+static uint32_t utilhash(uint32_t a) {
+  a = (a + 0x7ed55d16u) + (a << 12);
+  a = (a ^ 0xc761c23cu) ^ (a >> 19);
+  a = (a + 0x165667b1u) + (a << 5);
+  a = (a + 0xd3a2646cu) ^ (a << 9);
+  a = (a + 0xfd7046c5u) + (a << 3);
+  a = (a ^ 0xb55a4f09u) ^ (a >> 16);
+  return a;
+}
+static void rng_seeded(xorwow_t* s, uint32_t iteration, uint32_t index, uint32_t depth) {
+  const uint32_t h = utilhash(0x80000000u | (depth << 22) | iteration) ^ utilhash(index);
+  rng_init(s, (int32_t)h); /* Rng(int) */
+}
+
+/* NaiveVolPTmk_kernel.cuh:20-151 + NaiveVolPTmk::launchRender/extend
+ * (RenderKernelLauncher.cu:183-272).  Path id = iteration * tile_px + pixel,
+ * as for the other kernels.  d_init: camera ray from the (iteration, pixel,
+ * 0) stream, AABB test (a miss adds (1,1,1) to the pixel), GGX at the box
+ * before any medium test (Q12; a failed sample drops the path).  Each bounce
+ * (d_extend) re-seeds from (iteration, pixel, depth) and first draws three
+ * unused numbers (Q12), then runs one naiveSK segment (scatter with -eps).
+ * Compaction keeps every live path (Q11 fixed: the reference's
+ * `end - begin - 1` drops one live path per bounce).  Flags: bit0 contributed
+ * (T), bit1 truncated, bit2 missed the box at init (T = 1), bit3 dropped by a
+ * failed GGX sample at init.  n_segments counts d_init plus every d_extend. */
+static void trace_path_mk(const oracle_medium* m, const oracle_launch* L, uint32_t path_id, oracle_path* res) {
+  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
+  const uint32_t image_id = path_id % tile_px;
+  const uint32_t iteration = path_id / tile_px;
+  xorwow_t rng;
+  rng_seeded(&rng, iteration, image_id, 0u);
+  float px = (float)(image_id % (uint32_t)L->tile_res[0]) + (float)L->offset[0];
+  float py = det_floorf((float)image_id / L->tile_res[0]) + (float)L->offset[1];
+  f3 o, d;
+  camera_ray(L, px, py, &rng, &o, &d);
+  f3 T = mk3(1.0f, 1.0f, 1.0f);
+  memset(res, 0, sizeof(*res));
+  res->image_id = image_id;
+  res->n_segments = 1;
+  isect_t is;
+  is.dist = 0.0f;
+  is.normal = mk3(0, 0, 0);
+  is.inside = 0;
+  if (!aabb_intersect(m, o, d, &is)) {
+    res->flags = 1u | 4u;
+    res->T[0] = res->T[1] = res->T[2] = 1.0f;
+    return;
+  }
+  if (is.dist < 0.0f) is.dist = 0.0f; /* clamp to near plane */
+  o = add3(o, scl3(d, is.dist));
+  {
+    frame_t fr = frame_from_z(is.normal);
+    f3 dir = frame_to_local(&fr, normalize3(neg3(d)));
+    float weight = 1.0f;
+    if (!ggx_sample(m, dir, &rng, &d, &weight)) {
+      res->flags = 8u;
+      return;
+    }
+    T = scl3(T, weight);
+    d = frame_to_world(&fr, d);
+    o = add3(o, scl3(d, EPS));
+  }
+  for (uint32_t depth = 0;; ++depth) {
+    if (L->max_segments && res->n_segments >= L->max_segments) { res->flags |= 2u; break; }
+    ++res->n_segments;
+    rng_seeded(&rng, iteration, image_id, depth);
+    (void)rng_float(&rng); /* float3 e = rng.getFloat3(), unused */
+    (void)rng_float(&rng);
+    (void)rng_float(&rng);
+    is.dist = 0.0f; /* a fresh SimpleIsect per d_extend */
+    is.normal = mk3(0, 0, 0);
+    is.inside = 0;
+    if (!aabb_intersect(m, o, d, &is)) {
+      res->flags |= 1u;
+      break;
+    }
+    float sampled = 0.0f;
+    int collided = 0;
+    if (is.inside) {
+      sampled = woodcock(m, o, d, is.dist, &rng, &res->n_steps, &res->n_density);
+      collided = sampled < is.dist;
+    }
+    if (!collided) {
+      frame_t fr = frame_from_z(is.normal);
+      f3 dir = frame_to_local(&fr, normalize3(neg3(d)));
+      o = add3(o, scl3(d, is.dist));
+      float weight = 1.0f;
+      if (ggx_sample(m, dir, &rng, &d, &weight)) {
+        T = scl3(T, weight);
+        d = frame_to_world(&fr, d);
+        o = add3(o, scl3(d, EPS));
+      }
+    } else {
+      o = sub3(add3(o, scl3(d, sampled)), scl3(d, EPS));
+      f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
+      f3 bmax = mk3(m->box_max[0], m->box_max[1], m->box_max[2]);
+      f3 a = albedo_lookup(m, div3(sub3(o, bmin), sub3(bmax, bmin)));
+      ++res->n_albedo;
+      T = mul3(T, a);
+      float e1 = rng_float(&rng);
+      float e2 = rng_float(&rng);
+      d = hg_sample(d, m->g, e1, e2);
+    }
+    float p = det_fminf(1.0f, det_fmaxf(det_fmaxf(T.x, T.y), T.z));
+    if (rng_float(&rng) > p) break;
+    T = mk3(T.x / p, T.y / p, T.z / p);
+  }
+  res->T[0] = T.x;
+  res->T[1] = T.y;
+  res->T[2] = T.z;
+}
+
 /* ----------------------------------------------------------- path ------ */
 /* NaiveVolPTsk_kernel.cuh:17-87 (kernel 0) and
  * RegenerationVolPTsk_kernel.cuh:146-232 (kernel 2, no -eps at scatter, Q6).
  * `out` (optional) is the tile accumulator (float4 per pixel). */
 EXPORT void oracle_trace_path(const oracle_medium* m, const oracle_launch* L, uint32_t path_id,
                               oracle_path* res) {
+  if (L->kernel == 1) {
+    trace_path_mk(m, L, path_id, res);
+    return;
+  }
   const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
   const uint32_t image_id = path_id % tile_px;
   xorwow_t rng;

@@ -61,7 +61,7 @@ def test_rng_streams_golden(oracle_mod):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("key", list(CASES))
-@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK"])
+@pytest.mark.parametrize("kernel", ["naiveSK", "naiveMK", "regenerationSK"])
 def test_gpu_reproduces_golden(cvr, key, kernel):
     g = load(f"oracle_{key}.npz")
     W, H, iters, seed = (int(v) for v in g["meta"])

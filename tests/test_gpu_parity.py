@@ -77,7 +77,7 @@ def scenes(cvr):
 
 
 @pytest.mark.parametrize("scene_key", list(SCENES))
-@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK"])
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK", "naiveMK"])
 @pytest.mark.parametrize("cells", [1, 0])
 def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel, cells):
     scene = scenes[scene_key]
@@ -98,9 +98,11 @@ def test_per_path_bit_exact(cvr, oracle_mod, scenes, scene_key, kernel, cells):
     mism = np.nonzero((tb != cb).any(axis=1))[0]
     assert mism.size == 0, f"T bits differ for {mism.size} paths, first {mism[:5]}"
     assert c["n_density"].sum() > 0 and (c["flags"] & 1).any()
+    if kernel == "naiveMK":  # init misses (T = 1) and escapes after bounces both occur
+        assert ((c["flags"] & 4) != 0).any() and ((c["flags"] & 5) == 1).any()
 
 
-@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK", "sortingSK", "streamingMK"])
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK", "sortingSK", "streamingMK", "naiveMK"])
 @pytest.mark.parametrize("tiles", [(1, 1), (4, 2), (3, 3)])
 def test_render_image_matches_oracle(cvr, oracle_mod, scenes, kernel, tiles):
     scene = scenes["bucky"]
@@ -212,8 +214,8 @@ def test_c2_manix_1024_full_size_vs_oracle(cvr, oracle_mod):
 
 def test_errors_are_reported_not_fatal(cvr, scenes):
     with pytest.raises(cvr.CvrError) as e:
-        cvr.Context(0, "naiveMK")
-    assert "not implemented" in str(e.value)
+        cvr.Context(0, 9)
+    assert "unknown kernel" in str(e.value)
     ctx = cvr.Context(0, "regenerationSK")
     with pytest.raises(cvr.CvrError) as e:
         ctx.launch_render()

@@ -50,7 +50,7 @@ def main():
         iv, r2v = cvr.default_camera(W, H)
         arrays = {"meta": np.array([W, H, iters, seed], np.int64),
                   "scene_sha256": np.frombuffer(bytes.fromhex(scene_digest(s)), np.uint8)}
-        for kid in (0, 2):
+        for kid in (0, 1, 2):
             L = orc.launch(iv, r2v, (W, H), (W, H), (0, 0), kid, seed)
             rec = orc.trace_paths(L, 0, W * H * iters)
             arrays[f"paths_k{kid}"] = rec
