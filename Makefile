@@ -12,7 +12,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 OBJDIR := build/obj
 SRCS_HIP := $(CSRC)/cvr_kernels.hip $(CSRC)/cvr_persistent.hip $(CSRC)/cvr_pool.hip $(CSRC)/cvr_wpool.hip $(CSRC)/cvr_wavefront.hip
-SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp
+SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp $(CSRC)/cvr_mhd.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := include/cvr.h include/cvr_detmath.h $(wildcard $(CSRC)/*.h)
 
@@ -27,7 +27,7 @@ $(OBJDIR)/%.o: $(CSRC)/%.cpp $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
 
 $(PKG)/libcvr.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-soname,libcvr.so
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -Wl,-soname,libcvr.so -lz
 
 $(PKG)/cvr: $(CSRC)/cvr_main.cpp $(PKG)/libcvr.so include/cvr.h
 	g++ -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lcvr -Wl,-rpath,'$$ORIGIN'
@@ -48,5 +48,5 @@ clean:
 stamps: build/stamps/libcvr.so
 build/stamps/libcvr.so: $(SRCS_HIP) $(SRCS_CPP) $(HDRS)
 	@mkdir -p build/stamps
-	$(HIPCC) $(HIPFLAGS) -DCVR_STAMPS=1 -shared -o $@ $(SRCS_HIP) $(patsubst %,-x hip %,$(SRCS_CPP))
+	$(HIPCC) $(HIPFLAGS) -DCVR_STAMPS=1 -shared -o $@ $(SRCS_HIP) $(patsubst %,-x hip %,$(SRCS_CPP)) -lz
 .PHONY: stamps

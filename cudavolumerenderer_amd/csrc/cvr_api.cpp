@@ -37,6 +37,10 @@ int set_err(std::string* dst, int code, const char* fmt, ...) {
 
 }  // namespace
 
+namespace cvr {
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace cvr
+
 struct cvr_ctx {
   int device = 0;
   int kernel = CVR_KERNEL_REGENERATION_SK;

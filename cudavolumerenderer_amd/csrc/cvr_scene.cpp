@@ -264,6 +264,7 @@ int cvr_scene_synthetic(const char* name, uint32_t seed, const uint32_t* dims, c
   }
   if (r != CVR_OK) {
     delete s;
+    set_last_error("unknown synthetic scene " + nm);
     return r;
   }
   *out = s;
@@ -306,6 +307,8 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
   }
   if (r != CVR_OK) {
     delete s;
+    if (type == CVR_SCENE_VDB && r == CVR_ERR_IO) set_last_error(std::string("VDB: ") + vdb_last_error());
+    else set_last_error("cannot load scene " + p + (r == CVR_ERR_UNSUPPORTED ? " (unsupported)" : ""));
     return r;
   }
   *out = s;

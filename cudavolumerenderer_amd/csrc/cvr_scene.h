@@ -23,4 +23,6 @@ int scene_from_raw_bytes(const std::vector<uint8_t>& raw, const std::string& nam
 void finish_vdb_like(cvr_scene* s);
 int load_vdb_scene(const std::string& path, cvr_scene* s);
 int load_mhd_scene(const std::string& path, cvr_scene* s);
+const char* vdb_last_error();
+void set_last_error(const std::string& msg);  // cvr_last_error(NULL) text
 }  // namespace cvr
