@@ -12,7 +12,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 OBJDIR := build/obj
 SRCS_HIP := $(CSRC)/cvr_kernels.hip $(CSRC)/cvr_persistent.hip $(CSRC)/cvr_pool.hip $(CSRC)/cvr_wpool.hip $(CSRC)/cvr_wavefront.hip
-SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp $(CSRC)/cvr_mhd.cpp
+SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp $(CSRC)/cvr_mhd.cpp $(CSRC)/cvr_xml.cpp
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := include/cvr.h include/cvr_detmath.h $(wildcard $(CSRC)/*.h)
 

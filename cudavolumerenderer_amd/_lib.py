@@ -116,6 +116,7 @@ def load() -> C.CDLL:
         "cvr_scene_load": (I32, [C.c_char_p, I32, C.POINTER(P)]),
         "cvr_scene_synthetic": (I32, [C.c_char_p, U32, C.POINTER(U32), C.POINTER(P)]),
         "cvr_scene_medium": (I32, [P, C.POINTER(MediumDesc)]),
+        "cvr_scene_camera": (I32, [P, U32, U32, P, P]),
         "cvr_scene_raw_bytes": (I32, [P, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(C.c_size_t)]),
         "cvr_scene_destroy": (None, [P]),
         "cvr_write_hdr": (I32, [C.c_char_p, FP, U32, U32]),
@@ -194,6 +195,13 @@ class Scene:
         h = C.c_void_p()
         _check(lib.cvr_scene_load(path.encode(), SCENE_TYPES[scene_type], C.byref(h)))
         return cls(h)
+
+    def camera(self, width: int, height: int):
+        """(inv_view[12], raster_to_view[2]) of this scene's camera (cvr_scene_camera)."""
+        iv = np.zeros(12, np.float32)
+        r2v = np.zeros(2, np.float32)
+        _check(load().cvr_scene_camera(self._h, width, height, _fp(iv), _fp(r2v)))
+        return iv, r2v
 
     @property
     def dims(self):

@@ -39,6 +39,20 @@ int set_err(std::string* dst, int code, const char* fmt, ...) {
 
 namespace cvr {
 void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+// Camera(res, fov_x) then setResolution(w, h) -> setFovFromX (Camera.h:25-71),
+// and CudaVolPath::initCamera's rows of the model view (CudaVolPath.cpp:67-85).
+void camera_for_fov(float fov_x, uint32_t w, uint32_t h, float inv_view[12], float r2v[2]) {
+  const float fov_y = ((float)h / (float)w) * fov_x;
+  r2v[0] = tanf(fov_x * CVR_PI_F / 360.f);
+  r2v[1] = tanf(fov_y * CVR_PI_F / 360.f);
+  // glm column-major model view: col0 right (1,0,0,0) [MITSUBA_COMPARABLE],
+  // col1 up (0,-1,0,0), col2 view (0,0,-1,0), col3 position (0,0,100,1);
+  // initCamera takes rows of its transpose's first three rows.
+  const float mv[16] = {1, 0, 0, 0, 0, -1, 0, 0, 0, 0, -1, 0, 0, 0, 100.0f, 1};
+  const int idx[12] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14};
+  for (int i = 0; i < 12; ++i) inv_view[i] = mv[idx[i]];
+}
 }  // namespace cvr
 
 struct cvr_ctx {
@@ -863,17 +877,7 @@ done:
 // ------------------------------------------------------------- helpers ----
 int cvr_default_camera(uint32_t w, uint32_t h, float inv_view[12], float r2v[2]) {
   if (!inv_view || !r2v || w == 0 || h == 0) return set_err(nullptr, CVR_ERR_INVALID, "bad camera arguments");
-  // Camera(400,400,0.7) then setResolution(w,h) -> setFovFromX(fov.x)
-  const float fov_x = 0.7f;
-  const float fov_y = ((float)h / (float)w) * fov_x;
-  r2v[0] = tanf(fov_x * CVR_PI_F / 360.f);
-  r2v[1] = tanf(fov_y * CVR_PI_F / 360.f);
-  // glm column-major model view: col0 right (1,0,0,0) [MITSUBA_COMPARABLE],
-  // col1 up (0,-1,0,0), col2 view (0,0,-1,0), col3 position (0,0,100,1);
-  // initCamera takes rows of its transpose's first three rows.
-  const float mv[16] = {1, 0, 0, 0, 0, -1, 0, 0, 0, 0, -1, 0, 0, 0, 100.0f, 1};
-  const int idx[12] = {0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14};
-  for (int i = 0; i < 12; ++i) inv_view[i] = mv[idx[i]];
+  cvr::camera_for_fov(0.7f, w, h, inv_view, r2v);  // Camera(400, 400, 0.7), Camera.h:25
   return CVR_OK;
 }
 

@@ -147,7 +147,7 @@ int main(int argc, char** argv) {
     r = cvr_scene_load(o.scene_file.c_str(), st, &scene);
   }
   if (r != CVR_OK) {
-    fprintf(stderr, "Error: could not load scene (%d)\n", r);
+    fprintf(stderr, "Error: could not load scene (%d): %s\n", r, cvr_last_error(nullptr));
     return 1;
   }
   printf("[ConfigParser] kernel set to %s.\n[ConfigParser] iterations set to %u.\n", o.kernel.c_str(), o.iterations);
@@ -159,7 +159,7 @@ int main(int argc, char** argv) {
   cvr_scene_medium(scene, &md);
   const unsigned W = o.resolution[0], H = o.resolution[1];
   float inv_view[12], r2v[2];
-  cvr_default_camera(W, H, inv_view, r2v);
+  cvr_scene_camera(scene, W, H, inv_view, r2v);  // default camera; XML scenes carry their fov
   const float full_res[2] = {(float)W, (float)H};
   std::vector<float> image((size_t)W * H * 4, 0.0f);
   std::vector<double> times;

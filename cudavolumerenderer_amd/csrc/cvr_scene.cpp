@@ -302,13 +302,16 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
     r = load_vdb_scene(p, s);
   } else if (type == CVR_SCENE_MHD) {
     r = load_mhd_scene(p, s);
+  } else if (type == CVR_SCENE_MITSUBA_XML) {
+    r = load_xml_scene(p, s);
   } else {
     r = CVR_ERR_UNSUPPORTED;
   }
   if (r != CVR_OK) {
     delete s;
     if (type == CVR_SCENE_VDB && r == CVR_ERR_IO) set_last_error(std::string("VDB: ") + vdb_last_error());
-    else set_last_error("cannot load scene " + p + (r == CVR_ERR_UNSUPPORTED ? " (unsupported)" : ""));
+    else if (type != CVR_SCENE_MITSUBA_XML)
+      set_last_error("cannot load scene " + p + (r == CVR_ERR_UNSUPPORTED ? " (unsupported)" : ""));
     return r;
   }
   *out = s;
@@ -331,6 +334,12 @@ int cvr_scene_medium(const cvr_scene* s, cvr_medium_desc* m) {
   m->roughness[0] = 0.1f;     // GGX defaults (Bsdf.h:17-30)
   m->roughness[1] = 0.1f;
   m->eta = 1.05f / 1.01f;
+  return CVR_OK;
+}
+
+int cvr_scene_camera(const cvr_scene* s, uint32_t w, uint32_t h, float inv_view[12], float r2v[2]) {
+  if (!s || !inv_view || !r2v || w == 0 || h == 0) return CVR_ERR_INVALID;
+  cvr::camera_for_fov(s->fov_x, w, h, inv_view, r2v);
   return CVR_OK;
 }
 

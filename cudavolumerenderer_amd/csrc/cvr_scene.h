@@ -15,6 +15,7 @@ struct cvr_scene {
   float box_max[3] = {0.5f, 0.5f, 0.5f};
   float scale = 1.0f;
   float max_density = 1.0f;
+  float fov_x = 0.7f;        // camera horizontal fov in degrees (Camera.h:25; XML sensors set it)
   std::vector<uint8_t> raw;  // raw loader input bytes (for fixtures)
 };
 
@@ -23,6 +24,8 @@ int scene_from_raw_bytes(const std::vector<uint8_t>& raw, const std::string& nam
 void finish_vdb_like(cvr_scene* s);
 int load_vdb_scene(const std::string& path, cvr_scene* s);
 int load_mhd_scene(const std::string& path, cvr_scene* s);
+int load_xml_scene(const std::string& path, cvr_scene* s);
+void camera_for_fov(float fov_x, uint32_t w, uint32_t h, float inv_view[12], float r2v[2]);
 const char* vdb_last_error();
 void set_last_error(const std::string& msg);  // cvr_last_error(NULL) text
 }  // namespace cvr

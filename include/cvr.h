@@ -208,6 +208,12 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out);
 int cvr_scene_synthetic(const char* name, uint32_t seed, const uint32_t* dims, cvr_scene** out);
 /* Medium description; pointers stay owned by the scene. */
 int cvr_scene_medium(const cvr_scene* scene, cvr_medium_desc* out);
+/* The scene's camera at a render resolution: the fixed eye and orientation
+ * of Camera.h:25-45 with the scene's horizontal fov (0.7 degrees for VDB,
+ * Raw and MHD scenes; the XML sensor's fov, default 45, for Mitsuba scenes,
+ * XmlSceneBuilder.h:120-150). */
+int cvr_scene_camera(const cvr_scene* scene, uint32_t width, uint32_t height, float inv_view[12],
+                     float raster_to_view[2]);
 int cvr_scene_raw_bytes(const cvr_scene* scene, const uint8_t** bytes, size_t* n);
 void cvr_scene_destroy(cvr_scene* scene);
 /* Radiance RGBE .hdr of an RGBA float image (Image::saveHDR, Image.cpp:58-62). */

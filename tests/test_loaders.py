@@ -208,3 +208,50 @@ def test_reference_mhd_headers_parse_but_payloads_are_absent(cvr, tmp_path):
     (tmp_path / "manix_small.raw").write_text("version https://git-lfs.github.com/spec/v1\n")
     with pytest.raises(cvr.CvrError):
         cvr.Scene.load(str(tmp_path / "manix_small.mhd"))
+
+
+# ---------------------------------------------------------- Mitsuba XML --
+def _write_vol(path, data_zyxc, bbox):
+    nz, ny, nx, ch = data_zyxc.shape
+    head = b"VOL" + bytes([3]) + struct.pack("<iiiii", 1, nx, ny, nz, ch) + struct.pack("<6f", *bbox)
+    open(path, "wb").write(head + data_zyxc.astype("<f4").tobytes())
+
+
+def test_xml_scene_semantics(cvr, tmp_path):
+    """XmlSceneBuilder.h:39-266: density/albedo gridvolumes named in the XML,
+    scale from the XML, majorant max(min(1, v)) (Q15), AABB of the last file
+    read, i.e. the albedo (Q15), camera fov from the perspective sensor."""
+    rng = np.random.default_rng(5)
+    nz, ny, nx = 6, 7, 9
+    dens = rng.uniform(0, 1.6, (nz, ny, nx, 1)).astype(np.float32)
+    alb = rng.uniform(0, 1, (nz, ny, nx, 3)).astype(np.float32)
+    _write_vol(tmp_path / "d.vol", dens, (-1, -2, -3, 1, 2, 3))
+    _write_vol(tmp_path / "a.vol", alb, (-0.5, -0.25, 0, 0.5, 0.75, 2))
+    xml = open(os.path.join(GOLDEN, "hetvol.xml")).read()  # the reference's smoke scene, re-pointed
+    xml = xml.replace("smoke.vol", "d.vol").replace("albedo.vol", "a.vol").replace('value="800"', 'value="123.5"')
+    (tmp_path / "scene.xml").write_text(xml)
+    s = cvr.Scene.load(str(tmp_path / "scene.xml"))
+    assert s.dims == (nx, ny, nz)
+    assert np.array_equal(s.density, dens[..., 0])
+    assert np.array_equal(s.albedo[..., :3], alb) and (s.albedo[..., 3] == 1).all()
+    m = s.medium
+    assert m.scale == np.float32(123.5)
+    assert m.max_density == 1.0  # capped (Q15) although the grid goes to 1.6
+    assert tuple(m.box_min) == (-0.5, -0.25, 0.0) and tuple(m.box_max) == (0.5, 0.75, 2.0)
+    iv, r2v = s.camera(400, 200)
+    assert r2v[0] == pytest.approx(np.tan(0.33 * np.pi / 360), rel=1e-6)  # <float name="fov" value="0.33"/>
+    assert r2v[1] == pytest.approx(np.tan(0.33 * 0.5 * np.pi / 360), rel=1e-6)
+    assert list(iv) == list(cvr.default_camera(400, 200)[0])
+
+
+def test_xml_scene_errors(cvr, tmp_path):
+    # the reference's smoke scene: its .vol payloads are git-LFS pointers
+    (tmp_path / "hetvol.xml").write_text(open(os.path.join(GOLDEN, "hetvol.xml")).read())
+    (tmp_path / "smoke.vol").write_text("version https://git-lfs.github.com/spec/v1\n")
+    with pytest.raises(cvr.CvrError) as e:
+        cvr.Scene.load(str(tmp_path / "hetvol.xml"))
+    assert "smoke.vol" in str(e.value)
+    (tmp_path / "bad.xml").write_text("<scene><medium type='homogeneous'/></scene>")
+    with pytest.raises(cvr.CvrError) as e:
+        cvr.Scene.load(str(tmp_path / "bad.xml"))
+    assert "gridvolume" in str(e.value)
