@@ -50,3 +50,9 @@ build/stamps/libcvr.so: $(SRCS_HIP) $(SRCS_CPP) $(HDRS)
 	@mkdir -p build/stamps
 	$(HIPCC) $(HIPFLAGS) -DCVR_STAMPS=1 -shared -o $@ $(SRCS_HIP) $(patsubst %,-x hip %,$(SRCS_CPP)) -lz
 .PHONY: stamps
+
+# Experiment builds: make variant NAME=u2 DEFS="-DCVR_WPOOL_UNROLL=2" -> build/variants/u2/libcvr.so
+variant: $(SRCS_HIP) $(SRCS_CPP) $(HDRS)
+	@mkdir -p build/variants/$(NAME)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o build/variants/$(NAME)/libcvr.so $(SRCS_HIP) $(patsubst %,-x hip %,$(SRCS_CPP)) -lz
+.PHONY: variant

@@ -109,6 +109,7 @@ struct cvr_ctx {
   int pool_grid = 0;
   uint32_t pool_tail = 16;
   int wpool_grid = 0;
+  int wpool_waves = 4;  // wave-pool register/LDS budget: 4 or 5 waves per SIMD
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
@@ -255,7 +256,7 @@ int do_init(cvr_ctx* c) {
   if (pbpc < 1) pbpc = 1;
   c->pool_grid = pbpc * c->cu_count;
   int wbpc = 0;
-  HIP_TRY(c, cvr::wpool_occupancy(scatter_eps_for(c), &wbpc));
+  HIP_TRY(c, cvr::wpool_occupancy(scatter_eps_for(c), c->wpool_waves, &wbpc));
   if (wbpc < 1) wbpc = 1;
   c->wpool_grid = wbpc * c->cu_count;
   int tbpc = 0;
@@ -637,6 +638,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       if (v != 3 && v != 4 && v != 5 && v != 6 && v != 8)
         return set_err(&c->err, CVR_ERR_INVALID, "waves must be 3, 4, 5, 6 or 8");
       c->waves = (int)v;
+      c->wpool_waves = (v == 5) ? 5 : 4;
       c->inited = false;
       return CVR_OK;
     case CVR_OPT_BATCH:
@@ -707,7 +709,7 @@ int cvr_launch_render(cvr_ctx* c) {
     HIP_TRY(c, cvr::launch_pool(c->m, L, eps, grid, c->stream));
   } else if (scheduler_for(c) == 3) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->wpool_grid;
-    HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, grid, c->stream));
+    HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, c->wpool_waves, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }
@@ -773,10 +775,10 @@ int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   return CVR_OK;
 }
 
-int cvr_debug_counters(cvr_ctx* c, uint64_t out[8]) {
+int cvr_debug_counters(cvr_ctx* c, uint64_t out[16]) {
   if (!c || !out) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  HIP_TRY(c, hipMemcpy(out, c->d_work + kWorkDebug, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(out, c->d_work + kWorkDebug, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return CVR_OK;
 }
 

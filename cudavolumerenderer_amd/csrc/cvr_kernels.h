@@ -46,8 +46,9 @@ hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatt
                         hipStream_t s);
 hipError_t launch_pool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid, hipStream_t s);
 hipError_t pool_occupancy(bool scatter_eps, int* blocks_per_cu);
-hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid, hipStream_t s);
-hipError_t wpool_occupancy(bool scatter_eps, int* blocks_per_cu);
+hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
+                        hipStream_t s);
+hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);

@@ -31,15 +31,30 @@
 #ifndef CVR_STAMPS
 #define CVR_STAMPS 0
 #endif
+// Woodcock steps per track iteration between swap/event checks.
+#ifndef CVR_WPOOL_UNROLL
+#define CVR_WPOOL_UNROLL 3
+#endif
 
 namespace cvr {
 
 namespace {
 
-// Paths per wave (about 2 per lane).  125 keeps pool + launch parameters under
-// 10 KB so 16 single-wave workgroups (4 waves per SIMD) fit a CU's 160 KB LDS.
-constexpr int kSlots = 125;
+// Paths per wave for a register/LDS budget of kWaves waves per SIMD: pool +
+// launch parameters must fit 160 KB / (4 kWaves) of LDS (125 slots at 4 waves
+// per SIMD, 96 at 5).
+template <int kWaves>
+struct PoolSize;
+template <>
+struct PoolSize<4> {
+  static constexpr int value = 125;
+};
+template <>
+struct PoolSize<5> {
+  static constexpr int value = 96;
+};
 
+template <int kSlots>
 struct WavePool {
   float ox[kSlots], oy[kSlots], oz[kSlots], dx[kSlots], dy[kSlots], dz[kSlots];
   float tx[kSlots], ty[kSlots], tz[kSlots], dist[kSlots], t[kSlots];
@@ -64,7 +79,8 @@ __device__ __forceinline__ V3 normal_of(uint32_t c) {
   return c == 0u ? mk3(0, 0, 0) : c <= 2u ? mk3(s, 0, 0) : c <= 4u ? mk3(0, s, 0) : mk3(0, 0, s);
 }
 
-__device__ __forceinline__ void store_full(WavePool& S, uint32_t s, const PathState& ps, const Isect& is,
+template <int kSlots>
+__device__ __forceinline__ void store_full(WavePool<kSlots>& S, uint32_t s, const PathState& ps, const Isect& is,
                                            uint32_t nseg) {
   S.ox[s] = ps.o.x;
   S.oy[s] = ps.o.y;
@@ -86,7 +102,8 @@ __device__ __forceinline__ void store_full(WavePool& S, uint32_t s, const PathSt
   S.img[s] = ps.image_id;
   S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
 }
-__device__ __forceinline__ void load_full(const WavePool& S, uint32_t s, PathState& ps, Isect& is, uint32_t& nseg,
+template <int kSlots>
+__device__ __forceinline__ void load_full(const WavePool<kSlots>& S, uint32_t s, PathState& ps, Isect& is, uint32_t& nseg,
                                           float& t) {
   ps.o = mk3(S.ox[s], S.oy[s], S.oz[s]);
   ps.d = mk3(S.dx[s], S.dy[s], S.dz[s]);
@@ -100,7 +117,8 @@ __device__ __forceinline__ void load_full(const WavePool& S, uint32_t s, PathSta
   is.inside = (meta & 8u) != 0u;
   nseg = meta >> 4;
 }
-__device__ __forceinline__ void store_track(WavePool& S, uint32_t s, float t, const Rng& rng) {
+template <int kSlots>
+__device__ __forceinline__ void store_track(WavePool<kSlots>& S, uint32_t s, float t, const Rng& rng) {
   S.t[s] = t;
   S.r0[s] = rng.v0;
   S.r1[s] = rng.v1;
@@ -120,9 +138,10 @@ struct Cursor {
 
 }  // namespace
 
-template <bool kScatterEps>
-__global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk) {
-  __shared__ WavePool S;
+template <bool kScatterEps, int kWaves>
+__global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams m, LaunchParams Lk) {
+  constexpr int kSlots = PoolSize<kWaves>::value;
+  __shared__ WavePool<kSlots> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
   // scalars (v_readlane reloads in every Woodcock step).
@@ -139,8 +158,15 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
   uint32_t n_ln = kSlots;  // slots waiting for a new path (all of them at the start)
   for (uint32_t i = lane; i < (uint32_t)kSlots; i += 64u) S.ln[i] = (uint8_t)i;
 #if CVR_STAMPS
-  // event cycles, track cycles, event batches, track iterations, event-code cycles, regen+AABB cycles
-  unsigned long long st[6] = {0, 0, 0, 0, 0, 0};
+  // event cycles, track cycles, event batches, track iterations, event-code cycles, regen+AABB cycles,
+  // load, boundary, collision, regeneration cycles
+  unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define CVR_LAP(k)                                              \
+  {                                                             \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    st[k] += now_ - t_lap;                                      \
+    t_lap = now_;                                               \
+  }
   unsigned long long t_mark = __builtin_amdgcn_s_memtime();
 #endif
 
@@ -210,11 +236,14 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
 #if CVR_STAMPS
       ++st[3];
 #endif
-      if (slot >= 0 && !fin) {
-        const int r = woodcock_step(m, o, d, max_t, t, rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
-        if (r != 0) {
-          fin = true;
-          coll = (r == 2) && (t < max_t);
+#pragma unroll
+      for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
+        if (slot >= 0 && !fin) {
+          const int r = woodcock_step(m, o, d, max_t, t, rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
+          if (r != 0) {
+            fin = true;
+            coll = (r == 2) && (t < max_t);
+          }
         }
       }
     }
@@ -230,10 +259,14 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
     if (n_lb + n_lc == 0u && n_ready == 0u && (n_ln == 0u || cur.exhausted)) break;
 
     // ================================================= EVENT ==============
-    // One batch of up to 64 items, [boundary | collision | new] so each part
-    // runs one kind of code on consecutive lanes.  No item loops: a path
-    // that dies (roulette, escape, truncation) files its slot in the new
-    // list and is regenerated by a later batch.
+    // One batch of up to 64 items, [boundary | collision | new].  New items
+    // are regenerated first: a camera path's first segment is an AABB test
+    // and, when it hits the box from outside, a boundary event, which then
+    // runs in this batch's boundary part together with the filed boundary
+    // events.  Then the boundary part, the collision part (one kind of code
+    // each on consecutive lanes), and the AABB test of every survivor.  No
+    // item loops: a path that dies (roulette, escape, truncation) files its
+    // slot in the new list for a later batch.
     {
       const uint32_t tb = min(n_lb, 64u), tc = min(n_lc, 64u - tb), tn = min(n_ln, 64u - tb - tc);
       uint32_t kind = K_NONE, s = 0;
@@ -254,21 +287,15 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
       Isect is;
       uint32_t nseg = 0;
       float t_hit = 0.0f;
-      bool alive = false;
-      if (kind <= K_COLLIDE) load_full(S, s, ps, is, nseg, t_hit);
-      if (kind == K_BOUNDARY) {
-        boundary_event(m, ps, is);
-        alive = roulette(ps);
-      } else if (kind == K_COLLIDE) {
-        scatter_event<kScatterEps>(m, ps, t_hit);
-        ++c[STAT_ALBEDO];
-        alive = roulette(ps);
-      }
-      if (kind <= K_COLLIDE && !alive) seg_sum += nseg;
+      bool to_ready = false, to_lb = false, to_ln = false;
+#if CVR_STAMPS
+      unsigned long long t_lap = __builtin_amdgcn_s_memtime();
+#endif
       // ---- regeneration (new items): the wave's cursor into the global queues
       const unsigned long long want = __ballot(kind == K_NEW);
       if (want != 0ull) {
         const uint32_t rank = lane_rank(want);
+        bool got = false;
         uint32_t given = 0;  // new items [0, given) get a path
         while (given < (uint32_t)__popcll(want) && !cur.exhausted) {
           if (cur.next == cur.end) {
@@ -276,9 +303,9 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
             if (lane == 0) {
               for (uint32_t k = 0; k < L.n_queues; ++k) {
                 const uint32_t q = (cur.home + k) % L.n_queues;
-                const uint32_t got = atomicAdd(L.queue + 16 * q, L.chunk);
-                if (got < queue_units(L, q)) {
-                  b = got;
+                const uint32_t g = atomicAdd(L.queue + 16 * q, L.chunk);
+                if (g < queue_units(L, q)) {
+                  b = g;
                   qsel = q;
                   break;
                 }
@@ -299,15 +326,63 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
             path_begin(L, unit_to_path(L, cur.q, cur.next + (rank - given)), ps);
             is.normal = mk3(0, 0, 0);
             nseg = 0;
-            alive = true;
+            got = true;
             ++c[STAT_PATHS];
           }
           cur.next += take;
           given += take;
         }
+        // first segment: AABB test (NaiveVolPTsk_kernel.cuh:33-47); a new item
+        // that got no path (queues exhausted) leaves its slot empty
+        if (got) {
+          if (L.max_segments && nseg >= L.max_segments) {
+            ++c[STAT_TRUNCATED];
+            seg_sum += nseg;
+            to_ln = true;
+          } else {
+            ++nseg;
+            if (!aabb_intersect(m, ps.o, ps.d, is)) {
+              splat(L, ps);
+              ++c[STAT_ESCAPED];
+              seg_sum += nseg;
+              to_ln = true;
+            } else if (is.inside) {
+              store_full(S, s, ps, is, nseg);
+              to_ready = true;
+            } else {
+              kind = K_BOUNDARY;  // enters the box: boundary event in this batch
+            }
+          }
+        }
       }
-      // ---- next segment: AABB test (NaiveVolPTsk_kernel.cuh:33-47) -------
-      bool to_ready = false, to_lb = false, to_ln = false;
+#if CVR_STAMPS
+      CVR_LAP(9)
+#endif
+      if (lane < tb + tc) load_full(S, s, ps, is, nseg, t_hit);
+#if CVR_STAMPS
+      CVR_LAP(6)
+#endif
+      bool alive = false;
+      if (kind == K_BOUNDARY) {
+        boundary_event(m, ps, is);
+        alive = roulette(ps);
+      }
+#if CVR_STAMPS
+      CVR_LAP(7)
+#endif
+      if (kind == K_COLLIDE) {
+        scatter_event<kScatterEps>(m, ps, t_hit);
+        ++c[STAT_ALBEDO];
+        alive = roulette(ps);
+      }
+#if CVR_STAMPS
+      CVR_LAP(8)
+#endif
+      if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {
+        seg_sum += nseg;  // the path died in roulette
+        to_ln = true;
+      }
+      // ---- next segment: AABB test of the survivors ----------------------
       if (alive) {
         if (L.max_segments && nseg >= L.max_segments) {
           ++c[STAT_TRUNCATED];
@@ -326,10 +401,7 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
             to_lb = !is.inside;    // no medium: boundary at isect.dist
           }
         }
-      } else if (kind <= K_COLLIDE) {
-        to_ln = true;  // the path died in roulette
       }
-      // a new item that got no path (queues exhausted) leaves its slot empty
 #if CVR_STAMPS
       t_regen = __builtin_amdgcn_s_memtime();
 #endif
@@ -366,23 +438,28 @@ __global__ __launch_bounds__(64, 4) void k_wpool(MediumParams m, LaunchParams Lk
     st[1] += now - t_mark;
   }
   if (lane == 0)
-    for (int k = 0; k < 6; ++k) atomicAdd(L.stats + 16 + k, st[k]);
+    for (int k = 0; k < 10; ++k) atomicAdd(L.stats + 16 + k, st[k]);
 #endif
 }
 
-hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
-                        hipStream_t s) {
-  if (L.path_count == 0) return hipSuccess;
-  if (scatter_eps)
-    hipLaunchKernelGGL(k_wpool<true>, dim3(grid), dim3(64), 0, s, m, L);
-  else
-    hipLaunchKernelGGL(k_wpool<false>, dim3(grid), dim3(64), 0, s, m, L);
-  return hipGetLastError();
+template <bool E>
+static const void* wpool_fn(int waves) {
+  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5>);
+  return reinterpret_cast<const void*>(&k_wpool<E, 4>);
 }
 
-hipError_t wpool_occupancy(bool scatter_eps, int* blocks_per_cu) {
-  const void* fn = scatter_eps ? reinterpret_cast<const void*>(&k_wpool<true>)
-                               : reinterpret_cast<const void*>(&k_wpool<false>);
+hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
+                        hipStream_t s) {
+  if (L.path_count == 0) return hipSuccess;
+  const void* fn = scatter_eps ? wpool_fn<true>(waves) : wpool_fn<false>(waves);
+  MediumParams mm = m;
+  LaunchParams ll = L;
+  void* args[] = {&mm, &ll};
+  return hipLaunchKernel(fn, dim3(grid), dim3(64), args, 0, s);
+}
+
+hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu) {
+  const void* fn = scatter_eps ? wpool_fn<true>(waves) : wpool_fn<false>(waves);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, 0);
 }
 

@@ -172,7 +172,7 @@ int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_recor
 /* Diagnostic builds (-DCVR_STAMPS=1) only: per-phase cycle counters of the
  * persistent kernel {event cycles, track cycles, event phases, track
  * iterations}, summed over waves; zeros otherwise. */
-int cvr_debug_counters(cvr_ctx* ctx, uint64_t out[8]);
+int cvr_debug_counters(cvr_ctx* ctx, uint64_t out[16]);
 /* Device properties used for sizing: CU count, persistent grid. */
 int cvr_device_info(cvr_ctx* ctx, int* cu_count, int* persistent_grid);
 

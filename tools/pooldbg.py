@@ -14,5 +14,5 @@ for W, it, grid in [(32, 1, 1), (64, 1, 1), (64, 2, 0), (128, 4, 0)]:
     ctx.set_camera(iv, r2v, (W, W))
     ctx.init(); ctx.set_resolution(W, W); ctx.set_iterations(it)
     ctx.clear_output(); t = time.time(); ctx.launch_render(); st = ctx.stats()
-    out = (C.c_uint64 * 8)(); lib.cvr_debug_counters(ctx._h, out)
+    out = (C.c_uint64 * 16)(); lib.cvr_debug_counters(ctx._h, out)
     print(W, it, grid, 'ms', round((time.time() - t) * 1e3, 1), 'paths', st.paths, 'steps', st.steps, 'esc', st.escaped, 'dbg', list(out)[:4], flush=True)

@@ -30,7 +30,7 @@ for opts in [dict(), dict(ev=32), dict(tail=48)]:
     c.set_iterations(20)
     c.launch_render()
     st = c.stats()
-    out = (C.c_uint64 * 8)()
+    out = (C.c_uint64 * 16)()
     lib.cvr_debug_counters(c._h, out)
     ev, bev, tr, btr, n_it, n_rounds = list(out)[:6]
     tot = ev + bev + tr + btr

@@ -28,7 +28,7 @@ for ev in (56, 32, 16):
     c.set_iterations(20)
     c.launch_render()
     st = c.stats()
-    out = (C.c_uint64 * 8)()
+    out = (C.c_uint64 * 16)()
     lib.cvr_debug_counters(c._h, out)
     ev_c, tr_c, n_ev, n_tr = out[0], out[1], out[2], out[3]
     tot = ev_c + tr_c

@@ -50,7 +50,11 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--scene", default="manix")
     ap.add_argument("--variants", nargs="*", default=DEFAULT)
+    ap.add_argument("--lib", default=None, help="alternative libcvr.so (experiment builds)")
     a = ap.parse_args()
+    if a.lib:
+        import cudavolumerenderer_amd._lib as lb
+        lb.LIB_PATH = os.path.abspath(a.lib)
     scene = cvr.Scene.synthetic(a.scene)
     W = H = a.res
     iv, r2v = cvr.default_camera(W, H)

@@ -27,13 +27,15 @@ for batch in [8]:
     c.set_iterations(20)
     c.launch_render()
     st = c.stats()
-    out = (C.c_uint64 * 8)()
+    out = (C.c_uint64 * 16)()
     lib.cvr_debug_counters(c._h, out)
-    ev, tr, n_ev, n_tr, ev_code, ev_to_regen_end = list(out)[:6]
+    ev, tr, n_ev, n_tr, ev_code, ev_to_regen_end, c_load, c_bnd, c_col, c_regen = list(out)[:10]
     tot = ev + tr
     print(f"batch {batch}: kernel {st.kernel_ms:.2f} ms; event share {ev / tot:.3f}; event batches {n_ev} "
           f"({ev / max(n_ev, 1):.0f} cyc each, {(st.segments + st.paths) / max(n_ev, 1):.1f} items each); "
           f"track iterations {n_tr} ({tr / max(n_tr, 1):.0f} cyc each, {st.steps / max(n_tr, 1):.1f} lane-steps each); "
           f"per batch: load+event+roulette {ev_code / max(n_ev, 1):.0f}, regen+AABB+store "
-          f"{(ev_to_regen_end - ev_code) / max(n_ev, 1):.0f}, lists {(ev - ev_to_regen_end) / max(n_ev, 1):.0f} cyc",
+          f"{(ev_to_regen_end - ev_code) / max(n_ev, 1):.0f}, lists {(ev - ev_to_regen_end) / max(n_ev, 1):.0f} cyc; "
+          f"load {c_load / max(n_ev, 1):.0f} boundary {c_bnd / max(n_ev, 1):.0f} collision {c_col / max(n_ev, 1):.0f} "
+          f"regen {c_regen / max(n_ev, 1):.0f} AABB+store {(ev_to_regen_end - c_load - c_bnd - c_col - c_regen) / max(n_ev, 1):.0f}",
           flush=True)
