@@ -46,6 +46,10 @@ namespace {
 template <int kWaves>
 struct PoolSize;
 template <>
+struct PoolSize<3> {
+  static constexpr int value = 166;
+};
+template <>
 struct PoolSize<4> {
   static constexpr int value = 125;
 };
@@ -445,6 +449,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams m, LaunchPara
 template <bool E>
 static const void* wpool_fn(int waves) {
   if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5>);
+  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3>);
   return reinterpret_cast<const void*>(&k_wpool<E, 4>);
 }
 
