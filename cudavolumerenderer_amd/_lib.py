@@ -110,6 +110,7 @@ def load() -> C.CDLL:
         "cvr_trace_paths": (I32, [P, U32, U32, C.POINTER(PathRecord)]),
         "cvr_device_info": (I32, [P, C.POINTER(I32), C.POINTER(I32)]),
         "cvr_render_image": (I32, [P, C.POINTER(RenderDesc), P, FP, C.POINTER(Stats)]),
+        "cvr_render_tiles": (I32, [P, C.POINTER(RenderDesc), U32, U32, P, FP, C.POINTER(Stats)]),
         "cvr_default_camera": (I32, [U32, U32, FP, FP]),
         "cvr_tiling": (I32, [U32, U32, U32, U32, C.POINTER(U32)]),
         "cvr_tile_origin": (I32, [U32, U32, C.POINTER(U32), C.POINTER(U32)]),
@@ -356,13 +357,19 @@ class Context:
 
     def render_image(self, width, height, n_tiles=(1, 1), iterations=20, device_image: Optional[int] = None,
                      host: bool = True):
+        return self.render_tiles(width, height, n_tiles, iterations, 0, 1, device_image, host)
+
+    def render_tiles(self, width, height, n_tiles=(1, 1), iterations=20, first_tile: int = 0,
+                     tile_stride: int = 1, device_image: Optional[int] = None, host: bool = True):
+        """Tiles first_tile, first_tile + tile_stride, ... of render_image's
+        tile loop, each with its sequential-loop seed (cvr_render_tiles)."""
         d = RenderDesc()
         d.resolution[:] = (width, height)
         d.n_tiles[:] = n_tiles
         d.iterations = iterations
         st = Stats()
         img = np.zeros((height, width, 4), np.float32) if host else None
-        self._c(load().cvr_render_image(self._h, C.byref(d),
+        self._c(load().cvr_render_tiles(self._h, C.byref(d), first_tile, tile_stride,
                                         C.c_void_p(device_image) if device_image else None,
                                         _fp(img) if host else None, C.byref(st)))
         return img, st

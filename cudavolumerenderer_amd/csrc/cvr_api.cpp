@@ -724,17 +724,22 @@ int cvr_synchronize(cvr_ctx* c) {
   return CVR_OK;
 }
 
+// Per-tile seed advance (RenderKernelLauncher.cu): RegenerationVolPTsk and
+// StreamingVolPTmk add n_paths per reset (:359, :480), StreamingVolPTsk and
+// SortingVolPTsk add 1 (:573, :664), NaiveVolPTsk and NaiveVolPTmk keep it.
+// Returns the seed after `resets` resets starting from `seed` (u32 wrap).
+static uint32_t seed_after_resets(const cvr_ctx* c, uint32_t seed, uint32_t resets) {
+  if (c->kernel == CVR_KERNEL_REGENERATION_SK || c->kernel == CVR_KERNEL_STREAMING_MK)
+    return seed + (uint32_t)c->n_paths * resets;
+  if (c->kernel == CVR_KERNEL_STREAMING_SK || c->kernel == CVR_KERNEL_SORTING_SK) return seed + resets;
+  return seed;
+}
+
 int cvr_reset(cvr_ctx* c) {
   if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  // Per-tile seed advance (RenderKernelLauncher.cu): RegenerationVolPTsk and
-  // StreamingVolPTmk add n_paths (:359, :480), StreamingVolPTsk and
-  // SortingVolPTsk add 1 (:573, :664), NaiveVolPTsk only synchronises.
-  // Queue heads are re-zeroed per launch.
-  if (c->kernel == CVR_KERNEL_REGENERATION_SK || c->kernel == CVR_KERNEL_STREAMING_MK)
-    c->seed += (uint32_t)c->n_paths;
-  else if (c->kernel == CVR_KERNEL_STREAMING_SK || c->kernel == CVR_KERNEL_SORTING_SK)
-    c->seed += 1u;
+  // Queue heads are re-zeroed per launch; only the seed carries over.
+  c->seed = seed_after_resets(c, c->seed, 1);
   return CVR_OK;
 }
 
@@ -813,7 +818,13 @@ int cvr_trace_paths(cvr_ctx* c, uint32_t first, uint32_t count, cvr_path_record*
 
 // ------------------------------------------------------------ renderer ----
 int cvr_render_image(cvr_ctx* c, const cvr_render_desc* d, void* device_image, float* host_image, cvr_stats* stats) {
+  return cvr_render_tiles(c, d, 0, 1, device_image, host_image, stats);
+}
+
+int cvr_render_tiles(cvr_ctx* c, const cvr_render_desc* d, uint32_t first_tile, uint32_t tile_stride,
+                     void* device_image, float* host_image, cvr_stats* stats) {
   if (!c || !d) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (tile_stride == 0) return set_err(&c->err, CVR_ERR_INVALID, "tile stride 0");
   uint32_t tile_dim[2];
   int r = cvr_tiling(d->resolution[0], d->resolution[1], d->n_tiles[0], d->n_tiles[1], tile_dim);
   if (r) return set_err(&c->err, r, "%s", g_last_error.c_str());
@@ -829,10 +840,13 @@ int cvr_render_image(cvr_ctx* c, const cvr_render_desc* d, void* device_image, f
     HIP_TRY(c, hipMemsetAsync(tmp_img, 0, (size_t)W * H * sizeof(float4), c->stream));
     dimg = tmp_img;
   }
+  const uint32_t seed0 = c->seed;
   cvr_stats acc{};
   // initRenderState: memset the accumulator
   if ((r = cvr_clear_output(c))) goto done;
-  for (uint32_t k = 0; k < ntiles; ++k) {
+  for (uint32_t k = first_tile; k < ntiles; k += tile_stride) {
+    // the seed tile k has in the sequential tile loop (k resets after seed0)
+    c->seed = seed_after_resets(c, seed0, k);
     uint32_t org[2];
     cvr_tile_origin(k, d->n_tiles[0], tile_dim, org);
     if ((r = cvr_set_offset(c, org[0], org[1]))) goto done;  // copyOffset
@@ -859,6 +873,7 @@ int cvr_render_image(cvr_ctx* c, const cvr_render_desc* d, void* device_image, f
     if ((r = cvr_reset(c))) goto done;  // prepareForNextIterations
     if (ntiles != 1 && (r = cvr_clear_output(c))) goto done;
   }
+  c->seed = seed_after_resets(c, seed0, ntiles);  // as after the whole tile loop
   if (host_image) {
     hipError_t e = hipStreamSynchronize(c->stream);
     if (e == hipSuccess) e = hipMemcpy(host_image, dimg, (size_t)W * H * sizeof(float4), hipMemcpyDeviceToHost);

@@ -11,6 +11,13 @@ costs are very uneven (background vs volume).
 
 Weak scaling (bench.py): each rank renders its own `iterations` samples per
 pixel; the job renders iterations*world samples per pixel in total.
+
+Tile sharding (BASELINE C4, `--number-of-tiles 4 2` over 8 GPUs, tile k ->
+GPU k) is the reference's own decomposition and is kept as the second mode:
+rank r renders tiles r, r+world, ... of the tile loop with the seeds those
+tiles have in the sequential loop (cvr_render_tiles), into a zeroed full
+image, and the same one all-reduce concatenates the disjoint tiles.  Total
+work is fixed (strong scaling); its balance depends on the scene.
 """
 from __future__ import annotations
 
@@ -40,3 +47,29 @@ def render_sharded(render_range: Callable[[int, int], "object"], n_paths: int, r
     if world > 1 and all_reduce is not None:
         all_reduce(acc)
     return acc
+
+
+def tile_shard(n_tiles: int, rank: int, world: int) -> Tuple[int, int]:
+    """(first_tile, tile_stride) of rank `rank`: tiles rank, rank+world, ...
+    (tile k -> GPU k when n_tiles == world)."""
+    if world < 1 or not (0 <= rank < world) or n_tiles < 0:
+        raise ValueError(f"bad rank/world/tiles {rank}/{world}/{n_tiles}")
+    return rank, world
+
+
+def tiles_of(n_tiles: int, rank: int, world: int):
+    first, stride = tile_shard(n_tiles, rank, world)
+    return list(range(first, n_tiles, stride))
+
+
+def render_tiles_sharded(render_tiles: Callable[[int, int], "object"], n_tiles: int, rank: int, world: int,
+                         all_reduce: Callable[["object"], None] | None):
+    """Render this rank's tiles into a full, zeroed, normalised image, then
+    sum over ranks (tiles are disjoint, so the sum is the whole image).
+
+    `render_tiles(first_tile, tile_stride)` returns the rank's image."""
+    first, stride = tile_shard(n_tiles, rank, world)
+    img = render_tiles(first, stride)
+    if world > 1 and all_reduce is not None:
+        all_reduce(img)
+    return img

@@ -188,6 +188,14 @@ typedef struct cvr_render_desc {
  * Pixels outside tile_dim*n_tiles are not written (Q1). */
 int cvr_render_image(cvr_ctx* ctx, const cvr_render_desc* desc, void* device_image, float* host_image,
                      cvr_stats* stats);
+/* Tile-sharded variant (tile k -> GPU k): render only the
+ * tiles k = first_tile, first_tile + tile_stride, ... of the same tile loop,
+ * each with the seed it has in the full loop, so the per-rank images (zero
+ * elsewhere when `device_image` starts zeroed) sum to cvr_render_image's.
+ * The context's seed ends where the full loop leaves it.  Stats cover the
+ * rendered tiles.  cvr_render_image == cvr_render_tiles(ctx, desc, 0, 1, ...). */
+int cvr_render_tiles(cvr_ctx* ctx, const cvr_render_desc* desc, uint32_t first_tile, uint32_t tile_stride,
+                     void* device_image, float* host_image, cvr_stats* stats);
 
 /* ---- camera / tiling helpers ------------------------------------------ */
 /* Default Camera (Camera.h:25-71, MITSUBA_COMPARABLE) after

@@ -16,7 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from cudavolumerenderer_amd.distributed import render_sharded, shard_range
+from cudavolumerenderer_amd.distributed import render_sharded, render_tiles_sharded, shard_range, tiles_of
 
 W = H = 24
 ITERS = 3
@@ -88,3 +88,73 @@ def test_two_rank_gloo_render_equals_single(tmp_path):
     assert tuple(counts) == (st.steps, st.escaped, st.paths)
     bound = 2 * ITERS * 2.0 ** -24 * np.maximum(np.abs(img), np.abs(ref)) + 1e-30
     assert (np.abs(img[..., :3] - ref[..., :3]) <= bound[..., :3]).all()
+
+
+@pytest.mark.parametrize("n,world", [(8, 8), (8, 3), (9, 2), (1, 4), (0, 2)])
+def test_tile_shards_cover_each_tile_once(n, world):
+    tiles = sorted(t for r in range(world) for t in tiles_of(n, r, world))
+    assert tiles == list(range(n))
+    if n == world:  # tile k -> GPU k (C4)
+        assert all(tiles_of(n, r, world) == [r] for r in range(world))
+
+
+TW, TH, TILES = 32, 24, (4, 2)  # 8 tiles of 8x12
+
+
+def _tile_image(orc, iv, r2v, kernel, first, stride):
+    """The rank's tiles of the reference tile loop restated with the oracle,
+    each with its sequential-loop seed (RenderKernelLauncher.cu:359,573)."""
+    tw, th = TW // TILES[0], TH // TILES[1]
+    n_paths = tw * th * ITERS
+    img = np.zeros((TH, TW, 4), np.float32)
+    steps = 0
+    for k in range(first, TILES[0] * TILES[1], stride):
+        ox, oy = tw * (k % TILES[0]), th * (k // TILES[0])
+        sb = {2: k * n_paths, 4: k}.get(kernel, 0)
+        L = orc.launch(iv, r2v, (TW, TH), (tw, th), (ox, oy), kernel, sb)
+        tile, st = orc.render(L, 0, n_paths, nthreads=2)
+        img[oy:oy + th, ox:ox + tw] = tile / np.float32(ITERS)
+        steps += st.steps
+    return img, steps
+
+
+def _tile_worker(rank, world, port, outdir, kernel):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import cudavolumerenderer_amd as cvr
+        import oracle
+        s = cvr.Scene.synthetic("bucky")
+        orc = oracle.Oracle.from_medium_desc(s.medium, s.density, s.albedo)
+        iv, r2v = cvr.default_camera(TW, TH)
+        steps = [0]
+
+        def render_tiles(first, stride):
+            img, steps[0] = _tile_image(orc, iv, r2v, kernel, first, stride)
+            return torch.from_numpy(img)
+
+        img = render_tiles_sharded(render_tiles, TILES[0] * TILES[1], rank, world, lambda t: dist.all_reduce(t))
+        st = torch.tensor([steps[0]], dtype=torch.int64)
+        dist.all_reduce(st)
+        if rank == 0:
+            np.save(os.path.join(outdir, "img.npy"), img.numpy())
+            np.save(os.path.join(outdir, "steps.npy"), st.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kernel", [2, 4])  # regenerationSK (seed += n_paths), streamingSK (seed += 1)
+def test_two_rank_gloo_tile_sharding_equals_tile_loop(tmp_path, kernel):
+    mp.start_processes(_tile_worker, args=(2, _free_port(), str(tmp_path), kernel), nprocs=2, join=True,
+                       start_method="fork")
+    img = np.load(tmp_path / "img.npy")
+    steps = int(np.load(tmp_path / "steps.npy")[0])
+    import cudavolumerenderer_amd as cvr
+    import oracle
+    s = cvr.Scene.synthetic("bucky")
+    orc = oracle.Oracle.from_medium_desc(s.medium, s.density, s.albedo)
+    iv, r2v = cvr.default_camera(TW, TH)
+    ref, ref_steps = _tile_image(orc, iv, r2v, kernel, 0, 1)
+    assert steps == ref_steps
+    # disjoint tiles: the sum with zeros is exact
+    assert np.array_equal(np.nan_to_num(img), np.nan_to_num(ref))

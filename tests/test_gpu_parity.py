@@ -116,6 +116,34 @@ def test_render_image_matches_oracle(cvr, oracle_mod, scenes, kernel, tiles):
         assert getattr(st, k) == rst[k], k
 
 
+@pytest.mark.parametrize("kernel", ["naiveSK", "regenerationSK", "streamingSK", "streamingMK"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_render_tiles_sharded_sums_to_render_image(cvr, scenes, kernel, world):
+    """C4's decomposition: tile k -> rank k mod world (cvr_render_tiles).  The
+    ranks' images are disjoint and sum to the sequential tile loop's; every
+    rank's seed ends where the full loop leaves it."""
+    scene = scenes["manix_small"]
+    W, H, iters, tiles = 128, 96, 3, (4, 2)
+    ref, _, _ = make_ctx(cvr, scene, W, H, kernel, seed=11)
+    img0, st0 = ref.render_image(W, H, tiles, iters)
+    total = np.zeros_like(img0)
+    steps = paths = 0
+    for r in range(world):
+        ctx, _, _ = make_ctx(cvr, scene, W, H, kernel, seed=11)
+        img, st = ctx.render_tiles(W, H, tiles, iters, r, world)
+        mine = np.zeros((H, W), bool)
+        for k in range(r, 8, world):
+            ox, oy = (W // 4) * (k % 4), (H // 2) * (k // 4)
+            mine[oy:oy + H // 2, ox:ox + W // 4] = True
+        assert not np.nan_to_num(img)[~mine].any()
+        total += np.nan_to_num(img)
+        steps += st.steps
+        paths += st.paths
+        assert ctx.get_seed() == ref.get_seed()
+    assert steps == st0.steps and paths == st0.paths
+    assert_pixels_close(total, np.nan_to_num(img0), iters)
+
+
 def test_c1_bucky_256_4it(cvr, oracle_mod, scenes):
     """BASELINE config C1 (bucky 32^3, 256x256, 4 iterations) through naiveSK."""
     scene = scenes["bucky"]
