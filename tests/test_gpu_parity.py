@@ -240,6 +240,66 @@ def test_c2_manix_1024_full_size_vs_oracle(cvr, oracle_mod):
     assert_pixels_close(img, ref, 20)
 
 
+@pytest.mark.parametrize("kernel", ["regenerationSK", "streamingSK"])
+def test_c3_hetvol_1024_full_size_vs_oracle(cvr, oracle_mod, kernel):
+    """BASELINE config C3 at full size: hetvol proxy 128x128x50 (seed 800),
+    1024^2, Woodcock tracking through the regeneration and streaming
+    schedulers; the oracle renders the same paths on the host."""
+    scene = cvr.Scene.synthetic("hetvol")
+    W = H = 1024
+    iters = 8
+    ctx, iv, r2v = make_ctx(cvr, scene, W, H, kernel)
+    img, st = ctx.render_image(W, H, (1, 1), iters)
+    assert st.paths == W * H * iters and st.truncated == 0
+    ref, rst = oracle_image(oracle_mod, oracle_for(oracle_mod, scene), iv, r2v, W, H, (1, 1), iters,
+                            cvr.KERNELS.index(kernel))
+    for k in ("segments", "steps", "density", "albedo", "escaped"):
+        assert getattr(st, k) == rst[k], k
+    assert_pixels_close(img, ref, iters)
+
+
+def test_c4_manix_2048_256it_tiles_full_size(cvr, oracle_mod):
+    """BASELINE config C4 at full size: manix proxy, 2048^2, 256 iterations,
+    --number-of-tiles 4 2 (1.07 G paths).  Size-independent checks: the
+    8-way tile-sharded render (tile k -> rank k) sums to the sequential tile
+    loop with identical counters, and sampled path ranges of every tile are
+    bit-exact against the oracle with that tile's seed."""
+    scene = cvr.Scene.synthetic("manix")
+    W = H = 2048
+    iters, tiles = 256, (4, 2)
+    tw, th = W // 4, H // 2
+    n_paths = tw * th * iters
+    ref, iv, r2v = make_ctx(cvr, scene, W, H, "regenerationSK")
+    img0, st0 = ref.render_image(W, H, tiles, iters)
+    assert st0.paths == W * H * iters and st0.truncated == 0
+    total = np.zeros_like(img0)
+    steps = 0
+    for r in range(8):
+        ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+        img, st = ctx.render_tiles(W, H, tiles, iters, r, 8)
+        total += np.nan_to_num(img)
+        steps += st.steps
+        ctx.close()
+    assert steps == st0.steps
+    assert_pixels_close(total, np.nan_to_num(img0), iters)
+    orc = oracle_for(oracle_mod, scene)
+    ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
+    ctx.set_resolution(tw, th)
+    ctx.set_iterations(iters)
+    for k in range(8):
+        ox, oy = tw * (k % 4), th * (k // 4)
+        seed = (k * n_paths) & 0xFFFFFFFF
+        ctx.set_offset(ox, oy)
+        ctx.set_seed(seed)
+        L = orc.launch(iv, r2v, (W, H), (tw, th), (ox, oy), 2, seed)
+        for first in (0, n_paths // 2 + 12345, n_paths - 2048):
+            g = ctx.trace_paths(first, 2048)
+            c = orc.trace_paths(L, first, 2048)
+            for f in ("image_id", "flags", "n_segments", "n_steps", "n_density", "n_albedo"):
+                assert (g[f] == c[f]).all(), (k, first, f)
+            assert (g["T"].view(np.uint32) == c["T"].view(np.uint32)).all(), (k, first)
+
+
 def test_errors_are_reported_not_fatal(cvr, scenes):
     with pytest.raises(cvr.CvrError) as e:
         cvr.Context(0, 9)
