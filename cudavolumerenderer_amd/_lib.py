@@ -43,6 +43,18 @@ class MediumDesc(C.Structure):
                 ("g", C.c_float), ("roughness", C.c_float * 2), ("eta", C.c_float)]
 
 
+NO_LEAF = 0xFFFFFFFF
+
+
+class SparseMediumDesc(C.Structure):
+    _fields_ = [("res", C.c_uint32 * 3), ("leaf_dims", C.c_uint32 * 3),
+                ("leaf_table", C.POINTER(C.c_uint32)), ("n_leaves", C.c_uint32),
+                ("leaf_density", C.POINTER(C.c_float)), ("leaf_albedo", C.POINTER(C.c_float)),
+                ("albedo_background", C.c_float * 4), ("box_min", C.c_float * 3),
+                ("box_max", C.c_float * 3), ("scale", C.c_float), ("max_density", C.c_float),
+                ("g", C.c_float), ("roughness", C.c_float * 2), ("eta", C.c_float)]
+
+
 class Stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("steps", C.c_uint64),
                 ("density", C.c_uint64), ("albedo", C.c_uint64), ("escaped", C.c_uint64),
@@ -88,6 +100,9 @@ def load() -> C.CDLL:
         "cvr_destroy": (I32, [P]),
         "cvr_last_error": (C.c_char_p, [P]),
         "cvr_set_medium": (I32, [P, C.POINTER(MediumDesc)]),
+        "cvr_set_medium_sparse": (I32, [P, C.POINTER(SparseMediumDesc)]),
+        "cvr_scene_sparse_medium": (I32, [P, C.POINTER(SparseMediumDesc)]),
+        "cvr_scene_is_sparse": (I32, [P]),
         "cvr_set_camera": (I32, [P, FP, FP, FP]),
         "cvr_set_resolution": (I32, [P, U32, U32]),
         "cvr_set_offset": (I32, [P, U32, U32]),
@@ -179,8 +194,21 @@ class Scene:
 
     def __init__(self, handle):
         self._h = handle
-        self.medium = MediumDesc()
-        _check(load().cvr_scene_medium(self._h, C.byref(self.medium)))
+        self.is_sparse = bool(load().cvr_scene_is_sparse(self._h))
+        self._sparse = None
+        self.medium = None
+        if not self.is_sparse:
+            self.medium = MediumDesc()
+            _check(load().cvr_scene_medium(self._h, C.byref(self.medium)))
+
+    @property
+    def sparse_medium(self) -> SparseMediumDesc:
+        """8^3-leaf view (cvr_scene_sparse_medium; built once for dense scenes)."""
+        if self._sparse is None:
+            d = SparseMediumDesc()
+            _check(load().cvr_scene_sparse_medium(self._h, C.byref(d)))
+            self._sparse = d
+        return self._sparse
 
     @classmethod
     def synthetic(cls, name: str, seed: int = 0, dims: Optional[Sequence[int]] = None) -> "Scene":
@@ -206,16 +234,37 @@ class Scene:
 
     @property
     def dims(self):
-        return tuple(int(v) for v in self.medium.res)
+        return tuple(int(v) for v in (self.sparse_medium if self.is_sparse else self.medium).res)
+
+    def _dense_only(self):
+        if self.is_sparse:
+            raise CvrError(-5, "scene is stored sparse only (use leaves() / sparse_medium)")
+
+    @property
+    def max_density(self) -> float:
+        return float((self.sparse_medium if self.is_sparse else self.medium).max_density)
+
+    def leaves(self):
+        """(leaf_table (lz, ly, lx) u32, leaf_density (n, 8, 8, 8), leaf_albedo (n, 8, 8, 8, 4) or
+        None, albedo_background) as numpy views owned by the scene."""
+        d = self.sparse_medium
+        lx, ly, lz = (int(v) for v in d.leaf_dims)
+        table = np.ctypeslib.as_array(d.leaf_table, shape=(lz, ly, lx))
+        n = int(d.n_leaves)
+        dens = np.ctypeslib.as_array(d.leaf_density, shape=(n, 8, 8, 8)) if n else np.zeros((0, 8, 8, 8), np.float32)
+        alb = np.ctypeslib.as_array(d.leaf_albedo, shape=(n, 8, 8, 8, 4)) if (n and d.leaf_albedo) else None
+        return table, dens, alb, tuple(d.albedo_background)
 
     @property
     def density(self) -> np.ndarray:
         """(z, y, x) view of the fp32 density grid (owned by the scene)."""
+        self._dense_only()
         nx, ny, nz = self.dims
         return np.ctypeslib.as_array(self.medium.density, shape=(nz, ny, nx))
 
     @property
     def albedo(self) -> np.ndarray:
+        self._dense_only()
         nx, ny, nz = self.dims
         return np.ctypeslib.as_array(self.medium.albedo, shape=(nz, ny, nx, 4))
 
@@ -276,6 +325,9 @@ class Context:
 
     def set_medium(self, medium: MediumDesc):
         self._c(load().cvr_set_medium(self._h, C.byref(medium)))
+
+    def set_medium_sparse(self, desc: SparseMediumDesc):
+        self._c(load().cvr_set_medium_sparse(self._h, C.byref(desc)))
 
     def set_camera(self, inv_view, raster_to_view, full_res):
         iv = np.ascontiguousarray(inv_view, np.float32)

@@ -10,6 +10,7 @@
 //   TilingConfig + initTileArray                 Config.h:61-78, CudaVolPath.cpp:13-29
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -73,6 +74,12 @@ struct cvr_ctx {
   uint8_t* d_bounds = nullptr;  // brick bounds (MediumParams::bounds)
   uint32_t bound_shift = 2;     // log2 brick size, 0 = off
   size_t n_voxels = 0;
+  // sparse medium (cvr_set_medium_sparse)
+  uint32_t* d_leaves = nullptr;
+  float* d_leaf_density = nullptr;
+  float4* d_leaf_albedo = nullptr;
+  uint32_t* d_sbounds = nullptr;
+  size_t n_cell_leaves = 0;  // cell-leaf pool slots (incl. the zero slot)
   bool have_medium = false;
   cvr::MediumParams m{};
 
@@ -421,6 +428,8 @@ int cvr_create(int device, int kernel, cvr_ctx** out) {
   return CVR_OK;
 }
 
+static void free_sparse(cvr_ctx* c);
+
 int cvr_destroy(cvr_ctx* c) {
   if (!c) return CVR_OK;
   (void)hipSetDevice(c->device);
@@ -428,6 +437,8 @@ int cvr_destroy(cvr_ctx* c) {
   if (c->d_density) (void)hipFree(c->d_density);
   if (c->d_albedo) (void)hipFree(c->d_albedo);
   if (c->d_cells) (void)hipFree(c->d_cells);
+  if (c->d_bounds) (void)hipFree(c->d_bounds);
+  free_sparse(c);
   if (c->d_out_owned) (void)hipFree(c->d_out_owned);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -440,6 +451,45 @@ int cvr_destroy(cvr_ctx* c) {
   return CVR_OK;
 }
 
+static void free_sparse(cvr_ctx* c) {
+  if (c->d_leaves) (void)hipFree(c->d_leaves);
+  if (c->d_leaf_density) (void)hipFree(c->d_leaf_density);
+  if (c->d_leaf_albedo) (void)hipFree(c->d_leaf_albedo);
+  if (c->d_sbounds) (void)hipFree(c->d_sbounds);
+  c->d_leaves = nullptr;
+  c->d_leaf_density = nullptr;
+  c->d_leaf_albedo = nullptr;
+  c->d_sbounds = nullptr;
+  c->n_cell_leaves = 0;
+}
+
+// Geometry, scale and BSDF parameters shared by the dense and sparse uploads
+// (HeterogeneousMedium + GGX, Medium.h:110-190).
+static void fill_medium_common(cvr::MediumParams& m, const uint32_t res[3], const float box_min[3],
+                               const float box_max[3], float scale, float max_density, float g,
+                               const float roughness[2], float eta) {
+  m.rx = res[0];
+  m.ry = res[1];
+  m.rz = res[2];
+  m.fres_x = (float)res[0];
+  m.fres_y = (float)res[1];
+  m.fres_z = (float)res[2];
+  m.gx = (float)(res[0] - 1u);
+  m.gy = (float)(res[1] - 1u);
+  m.gz = (float)(res[2] - 1u);
+  m.bmin = cvr::V3{box_min[0], box_min[1], box_min[2]};
+  m.bmax = cvr::V3{box_max[0], box_max[1], box_max[2]};
+  const float ex = box_max[0] - box_min[0], ey = box_max[1] - box_min[1], ez = box_max[2] - box_min[2];
+  m.shift = cvr::V3{box_min[0] / ex, box_min[1] / ey, box_min[2] / ez};
+  m.scale = scale;
+  m.inv_sigma = 1.0f / (scale * max_density);
+  m.g = g;
+  m.ax = roughness[0];
+  m.ay = roughness[1];
+  m.eta = eta;
+  m.bq = (float)((1.0 / 254.0) * (1.0 + 1.0 / 65536.0));
+}
+
 int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   if (!c || !md) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   if (!md->density || !md->albedo) return set_err(&c->err, CVR_ERR_INVALID, "density/albedo is NULL");
@@ -449,7 +499,9 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   if (n > 0xFFFFFFFFull) return set_err(&c->err, CVR_ERR_INVALID, "grid exceeds 2^32 voxels");
   int r = ensure_device(c);
   if (r) return r;
-  if (n != c->n_voxels) {
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  free_sparse(c);
+  if (n != c->n_voxels || !c->d_density) {
     if (c->d_density) (void)hipFree(c->d_density);
     if (c->d_albedo) (void)hipFree(c->d_albedo);
     c->d_density = nullptr;
@@ -482,34 +534,116 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
   cvr::MediumParams& m = c->m;
+  m = cvr::MediumParams{};
   m.bounds = c->d_bounds;
   m.bshift = c->bound_shift;
   m.bnx = bnx;
   m.bny = bny;
-  m.bq = (float)((1.0 / 254.0) * (1.0 + 1.0 / 65536.0));
   m.cells = c->d_cells;
   m.density = c->d_density;
   m.albedo = c->d_albedo;
-  m.rx = md->res[0];
-  m.ry = md->res[1];
-  m.rz = md->res[2];
-  m.fres_x = (float)md->res[0];
-  m.fres_y = (float)md->res[1];
-  m.fres_z = (float)md->res[2];
-  m.gx = (float)(md->res[0] - 1u);
-  m.gy = (float)(md->res[1] - 1u);
-  m.gz = (float)(md->res[2] - 1u);
-  m.bmin = cvr::V3{md->box_min[0], md->box_min[1], md->box_min[2]};
-  m.bmax = cvr::V3{md->box_max[0], md->box_max[1], md->box_max[2]};
-  const float ex = md->box_max[0] - md->box_min[0], ey = md->box_max[1] - md->box_min[1],
-              ez = md->box_max[2] - md->box_min[2];
-  m.shift = cvr::V3{md->box_min[0] / ex, md->box_min[1] / ey, md->box_min[2] / ez};
-  m.scale = md->scale;
-  m.inv_sigma = 1.0f / (md->scale * md->max_density);
-  m.g = md->g;
-  m.ax = md->roughness[0];
-  m.ay = md->roughness[1];
-  m.eta = md->eta;
+  fill_medium_common(m, md->res, md->box_min, md->box_max, md->scale, md->max_density, md->g, md->roughness,
+                     md->eta);
+  c->have_medium = true;
+  return CVR_OK;
+}
+
+int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
+  if (!c || !sd) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  const uint32_t* res = sd->res;
+  if (res[0] == 0 || res[1] == 0 || res[2] == 0) return set_err(&c->err, CVR_ERR_INVALID, "empty grid");
+  for (int k = 0; k < 3; ++k)
+    if (sd->leaf_dims[k] != (res[k] + 7u) / 8u)
+      return set_err(&c->err, CVR_ERR_INVALID, "leaf_dims[%d] = %u, expected ceil(res/8) = %u", k, sd->leaf_dims[k],
+                     (res[k] + 7u) / 8u);
+  const uint32_t lnx = sd->leaf_dims[0], lny = sd->leaf_dims[1], lnz = sd->leaf_dims[2];
+  const size_t nleaf = (size_t)lnx * lny * lnz;
+  if (nleaf > 0xFFFFFFFFull) return set_err(&c->err, CVR_ERR_INVALID, "leaf table exceeds 2^32 entries");
+  if (!sd->leaf_table || (sd->n_leaves && !sd->leaf_density))
+    return set_err(&c->err, CVR_ERR_INVALID, "leaf table / density pool is NULL");
+  // cell leaves: a leaf's cells read the corners in it and its forward
+  // neighbours, so it needs a slot iff one of those 8 leaves exists
+  std::vector<uint32_t> cell_slot(nleaf, 0u), coords{0u, 0u, 0u};  // slot 0: the zero leaf
+  for (uint32_t z = 0; z < lnz; ++z)
+    for (uint32_t y = 0; y < lny; ++y)
+      for (uint32_t x = 0; x < lnx; ++x) {
+        const size_t i = ((size_t)z * lny + y) * lnx + x;
+        const uint32_t v = sd->leaf_table[i];
+        if (v != CVR_NO_LEAF && v >= sd->n_leaves)
+          return set_err(&c->err, CVR_ERR_INVALID, "leaf table entry %u >= n_leaves %u", v, sd->n_leaves);
+        bool any = false;
+        for (uint32_t dz = 0; dz < 2 && !any; ++dz)
+          for (uint32_t dy = 0; dy < 2 && !any; ++dy)
+            for (uint32_t dx = 0; dx < 2 && !any; ++dx)
+              if (x + dx < lnx && y + dy < lny && z + dz < lnz)
+                any = sd->leaf_table[((size_t)(z + dz) * lny + (y + dy)) * lnx + (x + dx)] != CVR_NO_LEAF;
+        if (any) {
+          cell_slot[i] = (uint32_t)(coords.size() / 3);
+          coords.insert(coords.end(), {x, y, z});
+        }
+      }
+  const size_t ncl = coords.size() / 3;
+  if (ncl > (1u << 24))
+    return set_err(&c->err, CVR_ERR_UNSUPPORTED, "sparse medium needs %zu cell leaves (> 2^24)", ncl);
+  int r = ensure_device(c);
+  if (r) return r;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // drop the previous medium (dense or sparse)
+  if (c->d_density) (void)hipFree(c->d_density);
+  if (c->d_albedo) (void)hipFree(c->d_albedo);
+  if (c->d_cells) (void)hipFree(c->d_cells);
+  if (c->d_bounds) (void)hipFree(c->d_bounds);
+  c->d_density = nullptr;
+  c->d_albedo = nullptr;
+  c->d_cells = nullptr;
+  c->d_bounds = nullptr;
+  c->n_voxels = 0;
+  c->have_medium = false;
+  free_sparse(c);
+  const size_t np = (size_t)sd->n_leaves * 512;
+  HIP_TRY(c, hipMalloc(&c->d_leaves, nleaf * sizeof(uint32_t)));
+  HIP_TRY(c, hipMemcpy(c->d_leaves, sd->leaf_table, nleaf * sizeof(uint32_t), hipMemcpyHostToDevice));
+  HIP_TRY(c, hipMalloc(&c->d_leaf_density, (np ? np : 1) * sizeof(float)));
+  if (np) HIP_TRY(c, hipMemcpy(c->d_leaf_density, sd->leaf_density, np * sizeof(float), hipMemcpyHostToDevice));
+  if (sd->leaf_albedo && np) {
+    HIP_TRY(c, hipMalloc(&c->d_leaf_albedo, np * sizeof(float4)));
+    HIP_TRY(c, hipMemcpy(c->d_leaf_albedo, sd->leaf_albedo, np * sizeof(float4), hipMemcpyHostToDevice));
+  }
+  cvr::MediumParams& m = c->m;
+  m = cvr::MediumParams{};
+  fill_medium_common(m, res, sd->box_min, sd->box_max, sd->scale, sd->max_density, sd->g, sd->roughness, sd->eta);
+  m.leaves = c->d_leaves;
+  m.leaf_density = c->d_leaf_density;
+  m.leaf_albedo = c->d_leaf_albedo;
+  m.lnx = lnx;
+  m.lny = lny;
+  m.albedo_bg = cvr::V3{sd->albedo_background[0], sd->albedo_background[1], sd->albedo_background[2]};
+  // bricks of 2^bshift <= 8 cells (within one leaf); bounds off -> q = 255
+  const float sigma = sd->scale * sd->max_density;
+  const int unbounded = !(c->bound_shift && sigma > 0.0f && std::isfinite(sigma) && sd->scale > 0.0f);
+  m.bshift = c->bound_shift == 0 ? 2u : std::min(c->bound_shift, 3u);
+  const uint32_t B = 1u << m.bshift;
+  m.bnx = (res[0] + B - 1) / B;
+  m.bny = (res[1] + B - 1) / B;
+  const uint32_t bnz = (res[2] + B - 1) / B;
+  const size_t nb = (size_t)m.bnx * m.bny * bnz;
+  HIP_TRY(c, hipMalloc(&c->d_sbounds, nb * sizeof(uint32_t)));
+  if (c->use_cells) HIP_TRY(c, hipMalloc(&c->d_cells, ncl * 1024 * sizeof(float4)));
+  uint32_t *d_coords = nullptr, *d_slot = nullptr;
+  hipError_t e = hipMalloc(&d_coords, coords.size() * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&d_slot, nleaf * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpy(d_coords, coords.data(), coords.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_slot, cell_slot.data(), nleaf * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = cvr::launch_build_sparse(m, d_coords, c->use_cells ? ncl : 0, d_slot, bnz, sd->max_density, unbounded,
+                                 c->d_cells, c->d_sbounds, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (d_coords) (void)hipFree(d_coords);
+  if (d_slot) (void)hipFree(d_slot);
+  if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "sparse medium build: %s", hipGetErrorString(e));
+  m.cells = c->d_cells;
+  m.sbounds = c->d_sbounds;
+  c->n_cell_leaves = ncl;
   c->have_medium = true;
   return CVR_OK;
 }

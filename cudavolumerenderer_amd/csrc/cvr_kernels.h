@@ -52,6 +52,12 @@ hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);
+// Sparse medium: cell-leaf pool (`coords`: 3 u32 leaf coordinates per slot,
+// slot 0 the zero leaf) and brick words (`cell_slot`: per leaf, its slot or 0).
+// `m` carries the leaf table/pools and the brick geometry (bshift <= 3).
+hipError_t launch_build_sparse(const MediumParams& m, const uint32_t* coords, size_t n_cell_leaves,
+                               const uint32_t* cell_slot, uint32_t bnz, float max_density, int unbounded,
+                               float4* cells, uint32_t* sbounds, hipStream_t s);
 hipError_t launch_build_cells(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, float4* cells,
                               hipStream_t s);
 hipError_t launch_tile_to_image(const float4* tile, uint32_t tw, uint32_t th, float4* image, uint32_t iw,

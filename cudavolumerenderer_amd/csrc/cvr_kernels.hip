@@ -220,6 +220,68 @@ __global__ __launch_bounds__(256) void k_build_bounds(const float* __restrict__ 
   }
 }
 
+// ------------------------------------------------------ sparse medium -----
+// Cell-leaf pool (MediumParams::cells for a sparse medium): slot s holds the
+// corner-replicated cells of leaf coords[s] (x, y, z leaf coordinates; slot 0
+// is the all-zero leaf).  Cells past the grid edge are never fetched (the
+// Woodcock range test) and are written as zeros.
+__global__ __launch_bounds__(256) void k_build_sparse_cells(MediumParams m, const uint32_t* __restrict__ coords,
+                                                            size_t n_cells, float4* __restrict__ cells) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n_cells; i += (size_t)gridDim.x * 256) {
+    const size_t slot = i >> 9;
+    const uint32_t local = (uint32_t)(i & 511u);
+    const uint32_t x = coords[3 * slot] * 8u + (local & 7u), y = coords[3 * slot + 1] * 8u + ((local >> 3) & 7u),
+                   z = coords[3 * slot + 2] * 8u + (local >> 6);
+    if (slot == 0 || x >= m.rx || y >= m.ry || z >= m.rz) {
+      cells[2 * i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      cells[2 * i + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
+    }
+    const uint32_t xb = min(x + 1, m.rx - 1), yb = min(y + 1, m.ry - 1), zb = min(z + 1, m.rz - 1);
+    cells[2 * i] = make_float4(texel_density(m, x, y, z), texel_density(m, xb, y, z), texel_density(m, x, yb, z),
+                               texel_density(m, xb, yb, z));
+    cells[2 * i + 1] = make_float4(texel_density(m, x, y, zb), texel_density(m, xb, y, zb),
+                                   texel_density(m, x, yb, zb), texel_density(m, xb, yb, zb));
+  }
+}
+
+// Sparse brick words: q << 24 | cell-leaf slot of the brick's leaf (bricks of
+// 2^bshift <= 8 cells never straddle leaves).  q as k_build_bounds; 0 for a
+// brick whose leaf has no cell slot (all its corners are 0), 255 everywhere
+// when `unbounded` (bounds off or no finite majorant: every point fetches).
+__global__ __launch_bounds__(256) void k_build_sparse_bounds(MediumParams m, const uint32_t* __restrict__ cell_slot,
+                                                             uint32_t bnz, float max_density, int unbounded,
+                                                             uint32_t* __restrict__ sb) {
+  const size_t nb = (size_t)m.bnx * m.bny * bnz;
+  const uint32_t B = 1u << m.bshift, up = 3u - m.bshift;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nb; i += (size_t)gridDim.x * 256) {
+    const uint32_t bx = (uint32_t)(i % m.bnx), by = (uint32_t)((i / m.bnx) % m.bny),
+                   bz = (uint32_t)(i / ((size_t)m.bnx * m.bny));
+    const uint32_t slot = cell_slot[((size_t)(bz >> up) * m.lny + (by >> up)) * m.lnx + (bx >> up)];
+    uint32_t v = 0u;
+    if (unbounded) {
+      v = 255u;
+    } else if (slot != 0u) {
+      const uint32_t x0 = bx * B, y0 = by * B, z0 = bz * B;
+      const uint32_t x1 = min(x0 + B, m.rx - 1), y1 = min(y0 + B, m.ry - 1), z1 = min(z0 + B, m.rz - 1);
+      float mx = 0.0f;
+      bool nan = false;
+      for (uint32_t z = z0; z <= z1; ++z)
+        for (uint32_t y = y0; y <= y1; ++y)
+          for (uint32_t x = x0; x <= x1; ++x) {
+            const float d = texel_density(m, x, y, z);
+            nan |= !(d == d) || d == __builtin_inff();
+            mx = fmaxf(mx, d);
+          }
+      const double r = (double)mx / (double)max_density;
+      if (nan || !(r <= 1.0)) v = 255u;
+      else if (mx == 0.0f) v = 0u;
+      else v = min(254u, (uint32_t)ceil(r * 254.0 * (1.0 + 1e-6)));
+    }
+    sb[i] = (v << 24) | slot;
+  }
+}
+
 // ---------------------------------------------------------- launchers -----
 hipError_t launch_naive(const MediumParams& m, const LaunchParams& L, bool scatter_eps, hipStream_t s) {
   if (L.path_count == 0) return hipSuccess;
@@ -269,6 +331,17 @@ hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, u
 hipError_t launch_build_cells(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, float4* cells,
                               hipStream_t s) {
   hipLaunchKernelGGL(k_build_cells, dim3(4096), dim3(256), 0, s, density, rx, ry, rz, cells);
+  return hipGetLastError();
+}
+
+hipError_t launch_build_sparse(const MediumParams& m, const uint32_t* coords, size_t n_cell_leaves,
+                               const uint32_t* cell_slot, uint32_t bnz, float max_density, int unbounded,
+                               float4* cells, uint32_t* sbounds, hipStream_t s) {
+  hipLaunchKernelGGL(k_build_sparse_cells, dim3(8192), dim3(256), 0, s, m, coords, n_cell_leaves * 512, cells);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_build_sparse_bounds, dim3(4096), dim3(256), 0, s, m, cell_slot, bnz, max_density, unbounded,
+                     sbounds);
   return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cvr.h"
@@ -241,6 +242,166 @@ static void synth_hetvol(cvr_scene* s, uint32_t seed, const uint32_t* dims) {
   finish_vdb_like(s);
 }
 
+// Cloud proxy: a sparse seeded fBm cumulus in a
+// 2048x1024x2048 index box, albedo (1,1,1), VDB-like (scale 100, unit AABB,
+// max_density = max voxel).  Stored sparse only: 8^3 leaves, the ones
+// holding a non-zero voxel.  In normalised coordinates p = (i + 0.5) / n the
+// density is clamp(2.5 (c(p) + 0.6 (fbm(6 p) - 0.5) - 0.1), 0, 1), where
+// c(p) = max_k (1 - |p - c_k| / r_k) over 28 seeded blobs; the fBm (4
+// octaves) is evaluated at the leaf corners and trilinearly interpolated
+// inside each leaf (its finest wavelength is ~5 leaves).
+struct CloudBlob {
+  double c[3], r;
+};
+
+static void synth_cloud(cvr_scene* s, uint32_t seed, const uint32_t* dims) {
+  const uint32_t nx = dims ? dims[0] : 2048, ny = dims ? dims[1] : 1024, nz = dims ? dims[2] : 2048;
+  s->name = "cloud";
+  s->dims[0] = nx;
+  s->dims[1] = ny;
+  s->dims[2] = nz;
+  const uint32_t lnx = (nx + 7) / 8, lny = (ny + 7) / 8, lnz = (nz + 7) / 8;
+  s->leaf_dims[0] = lnx;
+  s->leaf_dims[1] = lny;
+  s->leaf_dims[2] = lnz;
+  std::vector<CloudBlob> blobs(28);
+  uint32_t h = mix32(seed ^ 0x9e3779b9u);
+  auto uni = [&h](double a, double b) {
+    h = mix32(h + 0x6d2b79f5u);
+    return a + (b - a) * ((h >> 8) * (1.0 / 16777216.0));
+  };
+  for (auto& b : blobs) {
+    b.c[0] = uni(0.22, 0.78);
+    b.c[1] = uni(0.38, 0.62);
+    b.c[2] = uni(0.22, 0.78);
+    b.r = uni(0.07, 0.16);
+  }
+  const double leaf_rad = 0.5 * std::sqrt(std::pow(8.0 / nx, 2) + std::pow(8.0 / ny, 2) + std::pow(8.0 / nz, 2));
+  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  struct Part {
+    std::vector<uint32_t> leaf;
+    std::vector<float> vals;
+    float mx = 0.0f;
+  };
+  std::vector<Part> parts(nthreads);
+  auto work = [&](unsigned t) {
+    Part& P = parts[t];
+    const uint32_t z0 = (uint32_t)((uint64_t)lnz * t / nthreads), z1 = (uint32_t)((uint64_t)lnz * (t + 1) / nthreads);
+    std::vector<const CloudBlob*> near;
+    float v[512];
+    for (uint32_t lz = z0; lz < z1; ++lz)
+      for (uint32_t ly = 0; ly < lny; ++ly)
+        for (uint32_t lx = 0; lx < lnx; ++lx) {
+          const double pc[3] = {(lx * 8.0 + 4.0) / nx, (ly * 8.0 + 4.0) / ny, (lz * 8.0 + 4.0) / nz};
+          near.clear();
+          for (const auto& b : blobs) {
+            const double dx = pc[0] - b.c[0], dy = pc[1] - b.c[1], dz = pc[2] - b.c[2];
+            if (std::sqrt(dx * dx + dy * dy + dz * dz) < 1.2 * b.r + leaf_rad) near.push_back(&b);
+          }
+          if (near.empty()) continue;
+          double cn[2][2][2];  // fBm at the leaf corners
+          for (int a = 0; a < 2; ++a)
+            for (int bb = 0; bb < 2; ++bb)
+              for (int d = 0; d < 2; ++d)
+                cn[a][bb][d] = fbm(6.0 * (lx * 8.0 + 8 * d + 0.5) / nx, 6.0 * (ly * 8.0 + 8 * bb + 0.5) / ny,
+                                   6.0 * (lz * 8.0 + 8 * a + 0.5) / nz, 4, seed);
+          bool any = false;
+          for (uint32_t k = 0; k < 512; ++k) {
+            const uint32_t x = lx * 8 + (k & 7), y = ly * 8 + ((k >> 3) & 7), z = lz * 8 + (k >> 6);
+            float dv = 0.0f;
+            if (x < nx && y < ny && z < nz) {
+              const double p[3] = {(x + 0.5) / nx, (y + 0.5) / ny, (z + 0.5) / nz};
+              double cov = -1e30;
+              for (const CloudBlob* b : near) {
+                const double dx = p[0] - b->c[0], dy = p[1] - b->c[1], dz = p[2] - b->c[2];
+                cov = std::max(cov, 1.0 - std::sqrt(dx * dx + dy * dy + dz * dz) / b->r);
+              }
+              const double tx = (k & 7) / 8.0, ty = ((k >> 3) & 7) / 8.0, tz = (k >> 6) / 8.0;
+              auto L = [](double a, double b, double t) { return a + (b - a) * t; };
+              const double n = L(L(L(cn[0][0][0], cn[0][0][1], tx), L(cn[0][1][0], cn[0][1][1], tx), ty),
+                                 L(L(cn[1][0][0], cn[1][0][1], tx), L(cn[1][1][0], cn[1][1][1], tx), ty), tz);
+              const double d = 2.5 * (cov + 0.6 * (n - 0.5) - 0.1);
+              dv = (float)(d < 0 ? 0 : (d > 1 ? 1 : d));
+            }
+            v[k] = dv;
+            any |= dv != 0.0f;
+          }
+          if (!any) continue;
+          P.leaf.push_back((lz * lny + ly) * lnx + lx);
+          P.vals.insert(P.vals.end(), v, v + 512);
+          for (float x : v) P.mx = std::max(P.mx, x);
+        }
+  };
+  std::vector<std::thread> th;
+  for (unsigned t = 1; t < nthreads; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& t : th) t.join();
+  s->leaf_table.assign((size_t)lnx * lny * lnz, CVR_NO_LEAF);
+  size_t total = 0;
+  for (const auto& P : parts) total += P.leaf.size();
+  s->leaf_density.clear();
+  s->leaf_density.reserve(total * 512);
+  float mx = 0.0f;
+  uint32_t slot = 0;
+  for (auto& P : parts) {  // threads own ascending z ranges: slots follow the leaf index
+    for (uint32_t li : P.leaf) s->leaf_table[li] = slot++;
+    s->leaf_density.insert(s->leaf_density.end(), P.vals.begin(), P.vals.end());
+    mx = std::max(mx, P.mx);
+    std::vector<float>().swap(P.vals);
+  }
+  s->leaf_albedo.clear();
+  for (int k = 0; k < 4; ++k) s->albedo_bg[k] = 1.0f;
+  s->sparse_only = true;
+  s->have_leaves = true;
+  s->max_density = mx;
+  s->scale = 100.0f;
+  for (int k = 0; k < 3; ++k) {
+    s->box_min[k] = -0.5f;
+    s->box_max[k] = 0.5f;
+  }
+}
+
+// Dense grid -> 8^3 leaves: a leaf is stored when one of its voxels has a
+// density other than 0 or an albedo other than voxel (0,0,0)'s (the
+// background); the rest read as (0, background), exactly their values.
+static void build_leaves(cvr_scene* s) {
+  const uint32_t nx = s->dims[0], ny = s->dims[1], nz = s->dims[2];
+  const uint32_t lnx = (nx + 7) / 8, lny = (ny + 7) / 8, lnz = (nz + 7) / 8;
+  s->leaf_dims[0] = lnx;
+  s->leaf_dims[1] = lny;
+  s->leaf_dims[2] = lnz;
+  const float* bg = s->albedo.data();
+  memcpy(s->albedo_bg, bg, sizeof(s->albedo_bg));
+  s->leaf_table.assign((size_t)lnx * lny * lnz, CVR_NO_LEAF);
+  s->leaf_density.clear();
+  s->leaf_albedo.clear();
+  bool albedo_varies = false;
+  uint32_t slot = 0;
+  for (uint32_t lz = 0; lz < lnz; ++lz)
+    for (uint32_t ly = 0; ly < lny; ++ly)
+      for (uint32_t lx = 0; lx < lnx; ++lx) {
+        bool any = false;
+        for (uint32_t k = 0; k < 512 && !any; ++k) {
+          const uint32_t x = lx * 8 + (k & 7), y = ly * 8 + ((k >> 3) & 7), z = lz * 8 + (k >> 6);
+          if (x >= nx || y >= ny || z >= nz) continue;
+          const size_t i = ((size_t)z * ny + y) * nx + x;
+          any = s->density[i] != 0.0f || memcmp(&s->albedo[4 * i], bg, 16) != 0;
+        }
+        if (!any) continue;
+        s->leaf_table[((size_t)lz * lny + ly) * lnx + lx] = slot++;
+        for (uint32_t k = 0; k < 512; ++k) {
+          const uint32_t x = lx * 8 + (k & 7), y = ly * 8 + ((k >> 3) & 7), z = lz * 8 + (k >> 6);
+          const bool in = x < nx && y < ny && z < nz;
+          const size_t i = in ? ((size_t)z * ny + y) * nx + x : 0;
+          s->leaf_density.push_back(in ? s->density[i] : 0.0f);
+          for (int c = 0; c < 4; ++c) s->leaf_albedo.push_back(in ? s->albedo[4 * i + c] : bg[c]);
+          albedo_varies |= in && memcmp(&s->albedo[4 * i], bg, 16) != 0;
+        }
+      }
+  if (!albedo_varies) std::vector<float>().swap(s->leaf_albedo);
+  s->have_leaves = true;
+}
+
 }  // namespace cvr
 
 using namespace cvr;
@@ -259,6 +420,8 @@ int cvr_scene_synthetic(const char* name, uint32_t seed, const uint32_t* dims, c
     synth_manix(s, seed ? seed : 1234u, dims);
   } else if (nm == "hetvol") {
     synth_hetvol(s, seed ? seed : 800u, dims);
+  } else if (nm == "cloud") {
+    synth_cloud(s, seed ? seed : 5u, dims);
   } else {
     r = CVR_ERR_INVALID;
   }
@@ -321,6 +484,10 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
 int cvr_scene_medium(const cvr_scene* s, cvr_medium_desc* m) {
   if (!s || !m) return CVR_ERR_INVALID;
   memset(m, 0, sizeof(*m));
+  if (s->sparse_only) {
+    set_last_error("scene " + s->name + " is stored sparse only: use cvr_scene_sparse_medium");
+    return CVR_ERR_UNSUPPORTED;
+  }
   for (int k = 0; k < 3; ++k) {
     m->res[k] = s->dims[k];
     m->box_min[k] = s->box_min[k];
@@ -336,6 +503,35 @@ int cvr_scene_medium(const cvr_scene* s, cvr_medium_desc* m) {
   m->eta = 1.05f / 1.01f;
   return CVR_OK;
 }
+
+int cvr_scene_sparse_medium(cvr_scene* s, cvr_sparse_medium_desc* m) {
+  if (!s || !m) return CVR_ERR_INVALID;
+  memset(m, 0, sizeof(*m));
+  if (!s->have_leaves) {
+    if (s->density.empty() || s->albedo.size() != 4 * s->density.size()) return CVR_ERR_INVALID;
+    build_leaves(s);
+  }
+  for (int k = 0; k < 3; ++k) {
+    m->res[k] = s->dims[k];
+    m->leaf_dims[k] = s->leaf_dims[k];
+    m->box_min[k] = s->box_min[k];
+    m->box_max[k] = s->box_max[k];
+  }
+  m->leaf_table = s->leaf_table.data();
+  m->n_leaves = (uint32_t)(s->leaf_density.size() / 512);
+  m->leaf_density = s->leaf_density.data();
+  m->leaf_albedo = s->leaf_albedo.empty() ? nullptr : s->leaf_albedo.data();
+  memcpy(m->albedo_background, s->albedo_bg, sizeof(m->albedo_background));
+  m->scale = s->scale;
+  m->max_density = s->max_density;
+  m->g = 0.0f;
+  m->roughness[0] = 0.1f;
+  m->roughness[1] = 0.1f;
+  m->eta = 1.05f / 1.01f;
+  return CVR_OK;
+}
+
+int cvr_scene_is_sparse(const cvr_scene* s) { return s && s->sparse_only ? 1 : 0; }
 
 int cvr_scene_camera(const cvr_scene* s, uint32_t w, uint32_t h, float inv_view[12], float r2v[2]) {
   if (!s || !inv_view || !r2v || w == 0 || h == 0) return CVR_ERR_INVALID;

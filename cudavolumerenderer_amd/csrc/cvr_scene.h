@@ -17,6 +17,16 @@ struct cvr_scene {
   float max_density = 1.0f;
   float fov_x = 0.7f;        // camera horizontal fov in degrees (Camera.h:25; XML sensors set it)
   std::vector<uint8_t> raw;  // raw loader input bytes (for fixtures)
+  // Sparse storage (cvr_sparse_medium_desc): 8^3 leaves.  Filled by the
+  // sparse-only generators (sparse_only, density/albedo empty) or on demand
+  // from the dense grid by cvr_scene_sparse_medium.
+  bool sparse_only = false;
+  bool have_leaves = false;
+  uint32_t leaf_dims[3] = {0, 0, 0};
+  std::vector<uint32_t> leaf_table;
+  std::vector<float> leaf_density;  // 512 per leaf
+  std::vector<float> leaf_albedo;   // 512 * 4 per leaf, empty: albedo_bg everywhere
+  float albedo_bg[4] = {0.0f, 0.0f, 0.0f, 1.0f};
 };
 
 namespace cvr {

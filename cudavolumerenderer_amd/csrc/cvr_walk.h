@@ -89,6 +89,17 @@ struct MediumParams {
   const uint8_t* __restrict__ bounds;
   uint32_t bshift, bnx, bny;  // brick size log2, bricks per x / y row
   float bq;                   // (1/254)(1 + 2^-16): q -> bound on rho*inv_sigma
+  // Sparse storage (cvr_set_medium_sparse; all null for a dense medium):
+  // 8^3-voxel leaves, slot = leaves[leaf index] or CVR_NO_LEAF (density 0,
+  // albedo albedo_bg).  `density`/`albedo` are then null, `cells` is the
+  // cell-leaf pool (512 cells of 2 float4 per slot, slot 0 all zero) and
+  // `sbounds` replaces `bounds`: per brick, q << 24 | cell-leaf slot.
+  const uint32_t* __restrict__ leaves;
+  const float* __restrict__ leaf_density;  // slot * 512 + local
+  const float4* __restrict__ leaf_albedo;  // may be null: albedo_bg everywhere
+  const uint32_t* __restrict__ sbounds;
+  uint32_t lnx, lny;                       // leaves per x / y row
+  V3 albedo_bg;
   uint32_t rx, ry, rz;
   float fres_x, fres_y, fres_z;  // (float)res
   float gx, gy, gz;  // (float)(res-1): DeviceVolume::volumeToGrid
@@ -200,35 +211,35 @@ CVR_DEV float trilerp8(float d000, float d001, float d010, float d011, float d10
   return lerpf(a, b, fz, _fz);
 }
 
-CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p);
-
-// Woodcock density evaluation: cell path when the lower corner is inside the
-// grid (the overwhelmingly common case), else the 8-tap gather.
-CVR_DEV float density_lookup(const MediumParams& m, V3 p) {
-  if (m.cells) {
-    const float cx = p.x * m.gx, cy = p.y * m.gy, cz = p.z * m.gz;
-    // floor in float; for 0 <= f < res the int conversion is exact, so this
-    // equals det_floor_i32 + the uint range test (NaN fails the test).
-    const float fx1 = __builtin_floorf(cx), fy1 = __builtin_floorf(cy), fz1 = __builtin_floorf(cz);
-    if (fx1 >= 0.0f && fx1 < m.fres_x && fy1 >= 0.0f && fy1 < m.fres_y && fz1 >= 0.0f && fz1 < m.fres_z) {
-      const uint32_t x1 = (uint32_t)fx1, y1 = (uint32_t)fy1, z1 = (uint32_t)fz1;
-      const uint32_t cell = (__umul24(z1, m.ry) + y1) * m.rx + x1;
-      const float4 lo = m.cells[2 * cell], hi = m.cells[2 * cell + 1];
-      return trilerp8(lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, cx - fx1, cy - fy1, cz - fz1);
-    }
+// Texel fetch from the dense grid or the sparse leaves (same value).
+CVR_DEV uint32_t leaf_local(uint32_t x, uint32_t y, uint32_t z) {
+  return ((z & 7u) << 6) | ((y & 7u) << 3) | (x & 7u);
+}
+CVR_DEV float texel_density(const MediumParams& m, uint32_t x, uint32_t y, uint32_t z) {
+  if (m.leaves) {
+    const uint32_t slot = m.leaves[(__umul24(z >> 3, m.lny) + (y >> 3)) * m.lnx + (x >> 3)];
+    return slot == 0xFFFFFFFFu ? 0.0f : m.leaf_density[((size_t)slot << 9) | leaf_local(x, y, z)];
   }
-  return density_lookup_gather(m, p);
+  return m.density[(z * m.ry + y) * m.rx + x];
+}
+CVR_DEV float4 texel_albedo(const MediumParams& m, uint32_t x, uint32_t y, uint32_t z) {
+  if (m.leaves) {
+    const uint32_t slot = m.leaf_albedo ? m.leaves[(__umul24(z >> 3, m.lny) + (y >> 3)) * m.lnx + (x >> 3)]
+                                        : 0xFFFFFFFFu;
+    return slot == 0xFFFFFFFFu ? make_float4(m.albedo_bg.x, m.albedo_bg.y, m.albedo_bg.z, 1.0f)
+                               : m.leaf_albedo[((size_t)slot << 9) | leaf_local(x, y, z)];
+  }
+  return m.albedo[(z * m.ry + y) * m.rx + x];
 }
 
+// The reference's 8-tap trilinear (Volume.h:47-69), used where no cell
+// applies (the Q5 wrap, points outside the grid).
 CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p) {
   const Tri t = tri_setup(m, p);
-  const float* __restrict__ D = m.density;
-  const uint32_t r00 = (t.za * m.ry + t.ya) * m.rx, r01 = (t.za * m.ry + t.yb) * m.rx;
-  const uint32_t r10 = (t.zb * m.ry + t.ya) * m.rx, r11 = (t.zb * m.ry + t.yb) * m.rx;
-  const float d000 = D[r00 + t.xa], d001 = D[r00 + t.xb];
-  const float d010 = D[r01 + t.xa], d011 = D[r01 + t.xb];
-  const float d100 = D[r10 + t.xa], d101 = D[r10 + t.xb];
-  const float d110 = D[r11 + t.xa], d111 = D[r11 + t.xb];
+  const float d000 = texel_density(m, t.xa, t.ya, t.za), d001 = texel_density(m, t.xb, t.ya, t.za);
+  const float d010 = texel_density(m, t.xa, t.yb, t.za), d011 = texel_density(m, t.xb, t.yb, t.za);
+  const float d100 = texel_density(m, t.xa, t.ya, t.zb), d101 = texel_density(m, t.xb, t.ya, t.zb);
+  const float d110 = texel_density(m, t.xa, t.yb, t.zb), d111 = texel_density(m, t.xb, t.yb, t.zb);
   const float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
   const float a = lerpf(lerpf(d000, d001, t.fx, _fx), lerpf(d010, d011, t.fx, _fx), t.fy, _fy);
   const float b = lerpf(lerpf(d100, d101, t.fx, _fx), lerpf(d110, d111, t.fx, _fx), t.fy, _fy);
@@ -236,13 +247,10 @@ CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p) {
 }
 CVR_DEV V3 albedo_lookup(const MediumParams& m, V3 p) {
   const Tri t = tri_setup(m, p);
-  const float4* __restrict__ A = m.albedo;
-  const uint32_t r00 = (t.za * m.ry + t.ya) * m.rx, r01 = (t.za * m.ry + t.yb) * m.rx;
-  const uint32_t r10 = (t.zb * m.ry + t.ya) * m.rx, r11 = (t.zb * m.ry + t.yb) * m.rx;
-  const float4 d000 = A[r00 + t.xa], d001 = A[r00 + t.xb];
-  const float4 d010 = A[r01 + t.xa], d011 = A[r01 + t.xb];
-  const float4 d100 = A[r10 + t.xa], d101 = A[r10 + t.xb];
-  const float4 d110 = A[r11 + t.xa], d111 = A[r11 + t.xb];
+  const float4 d000 = texel_albedo(m, t.xa, t.ya, t.za), d001 = texel_albedo(m, t.xb, t.ya, t.za);
+  const float4 d010 = texel_albedo(m, t.xa, t.yb, t.za), d011 = texel_albedo(m, t.xb, t.yb, t.za);
+  const float4 d100 = texel_albedo(m, t.xa, t.ya, t.zb), d101 = texel_albedo(m, t.xb, t.ya, t.zb);
+  const float4 d110 = texel_albedo(m, t.xa, t.yb, t.zb), d111 = texel_albedo(m, t.xb, t.yb, t.zb);
   const float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
 #define CVR_TRI(c)                                                                     \
   lerpf(lerpf(lerpf(d000.c, d001.c, t.fx, _fx), lerpf(d010.c, d011.c, t.fx, _fx), t.fy, \
@@ -312,16 +320,23 @@ CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float&
   const bool in = (fx1 >= 0.0f) & (fx1 < m.fres_x) & (fy1 >= 0.0f) & (fy1 < m.fres_y) & (fz1 >= 0.0f) &
                   (fz1 < m.fres_z);
   const uint32_t x1 = in ? (uint32_t)fx1 : 0u, y1 = in ? (uint32_t)fy1 : 0u, z1 = in ? (uint32_t)fz1 : 0u;
-  if (m.bounds) {
-    const uint32_t bi = (__umul24(z1 >> m.bshift, m.bny) + (y1 >> m.bshift)) * m.bnx + (x1 >> m.bshift);
-    const uint32_t q = in ? (uint32_t)m.bounds[bi] : 255u;
-    if ((float)q * m.bq < xi_test) return 0;
+  const uint32_t bi = (__umul24(z1 >> m.bshift, m.bny) + (y1 >> m.bshift)) * m.bnx + (x1 >> m.bshift);
+  const float4* cp;
+  if (m.sbounds) {  // sparse: bound and cell-leaf slot in one word
+    const uint32_t e = in ? m.sbounds[bi] : 0xFF000000u;
+    if ((float)(e >> 24) * m.bq < xi_test) return 0;
+    cp = m.cells + ((((size_t)(e & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
+  } else {
+    if (m.bounds) {
+      const uint32_t q = in ? (uint32_t)m.bounds[bi] : 255u;
+      if ((float)q * m.bq < xi_test) return 0;
+    }
+    cp = m.cells + 2 * ((__umul24(z1, m.ry) + y1) * m.rx + x1);
   }
   ++n_fetch;
   float dens;
   if (in && m.cells) {
-    const uint32_t cell = (__umul24(z1, m.ry) + y1) * m.rx + x1;
-    const float4 lo = m.cells[2 * cell], hi = m.cells[2 * cell + 1];
+    const float4 lo = cp[0], hi = cp[1];
     dens = trilerp8(lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, cx - fx1, cy - fy1, cz - fz1);
   } else {
     dens = density_lookup_gather(m, c);

@@ -142,9 +142,18 @@ struct Cursor {
 
 }  // namespace
 
-template <bool kScatterEps, int kWaves>
-__global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams m, LaunchParams Lk) {
+template <bool kScatterEps, int kWaves, bool kSparse>
+__global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr int kSlots = PoolSize<kWaves>::value;
+  // Dense instances see the sparse pointers as constant null, so the sparse
+  // branches of the walk code fold away and take no scalar registers.
+  MediumParams m = mk;
+  if constexpr (!kSparse) {
+    m.leaves = nullptr;
+    m.leaf_density = nullptr;
+    m.leaf_albedo = nullptr;
+    m.sbounds = nullptr;
+  }
   __shared__ WavePool<kSlots> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
@@ -447,16 +456,18 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams m, LaunchPara
 }
 
 template <bool E>
-static const void* wpool_fn(int waves) {
-  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5>);
-  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3>);
-  return reinterpret_cast<const void*>(&k_wpool<E, 4>);
+static const void* wpool_fn(int waves, bool sparse) {
+  if (sparse) return reinterpret_cast<const void*>(&k_wpool<E, 4, true>);
+  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false>);
+  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false>);
+  return reinterpret_cast<const void*>(&k_wpool<E, 4, false>);
 }
 
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
                         hipStream_t s) {
   if (L.path_count == 0) return hipSuccess;
-  const void* fn = scatter_eps ? wpool_fn<true>(waves) : wpool_fn<false>(waves);
+  const bool sparse = m.leaves != nullptr;
+  const void* fn = scatter_eps ? wpool_fn<true>(waves, sparse) : wpool_fn<false>(waves, sparse);
   MediumParams mm = m;
   LaunchParams ll = L;
   void* args[] = {&mm, &ll};
@@ -464,7 +475,7 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
 }
 
 hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu) {
-  const void* fn = scatter_eps ? wpool_fn<true>(waves) : wpool_fn<false>(waves);
+  const void* fn = scatter_eps ? wpool_fn<true>(waves, false) : wpool_fn<false>(waves, false);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, 0);
 }
 

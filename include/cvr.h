@@ -92,6 +92,33 @@ typedef struct cvr_medium_desc {
   float eta;              /* int_ior / ext_ior (1.05f / 1.01f) */
 } cvr_medium_desc;
 
+/* Sparse medium (extension): the grid of cvr_medium_desc
+ * stored as 8^3-voxel leaves (the OpenVDB leaf size).  Voxel (x,y,z) is
+ * leaf_density[slot*512 + ((z&7)*8 + (y&7))*8 + (x&7)] with
+ * slot = leaf_table[((z>>3)*leaf_dims[1] + (y>>3))*leaf_dims[0] + (x>>3)];
+ * a slot of CVR_NO_LEAF means density 0 and albedo albedo_background for
+ * all 512 voxels.  Rendering is identical to cvr_set_medium on the densified
+ * grid: only the storage differs.  Replaces the reference's dense textures
+ * (CudaVolPath.cpp:117-186) where they do not fit (a 2048x1024x2048 cloud is
+ * 17 GB of fp32 density + 69 GB of float4 albedo dense). */
+#define CVR_NO_LEAF 0xFFFFFFFFu
+typedef struct cvr_sparse_medium_desc {
+  uint32_t res[3];             /* index-space grid resolution (as cvr_medium_desc.res) */
+  uint32_t leaf_dims[3];       /* ceil(res / 8) */
+  const uint32_t* leaf_table;  /* host, leaf_dims product entries, x fastest: slot or CVR_NO_LEAF */
+  uint32_t n_leaves;           /* slots in the pools */
+  const float* leaf_density;   /* host, n_leaves * 512 fp32 */
+  const float* leaf_albedo;    /* host, n_leaves * 512 * 4 fp32 (r,g,b,1), or NULL: albedo_background everywhere */
+  float albedo_background[4];  /* albedo outside the leaves */
+  float box_min[3];
+  float box_max[3];
+  float scale;
+  float max_density;
+  float g;
+  float roughness[2];
+  float eta;
+} cvr_sparse_medium_desc;
+
 typedef struct cvr_stats {
   uint64_t paths;      /* paths started */
   uint64_t segments;   /* loop iterations (RAYS_STATISTICS count) */
@@ -126,6 +153,10 @@ int cvr_abi_version(void);
 /* setScene + createTextureWithVolume (CudaVolPath.cpp:88-186): copies the
  * host volumes into HBM (the caller keeps ownership of the host arrays). */
 int cvr_set_medium(cvr_ctx* ctx, const cvr_medium_desc* medium);
+/* Sparse upload: leaf pools go to HBM as they are; the density cells and
+ * brick bounds are built on the device for the leaves whose cells can
+ * interpolate a non-zero density (a brick-pool instead of dense cells). */
+int cvr_set_medium_sparse(cvr_ctx* ctx, const cvr_sparse_medium_desc* medium);
 /* copyInvViewMatrix (12 floats), copyRasterToView, copyPixelIndexRange */
 int cvr_set_camera(cvr_ctx* ctx, const float inv_view[12], const float raster_to_view[2],
                    const float full_res[2]);
@@ -211,11 +242,21 @@ int cvr_tile_origin(uint32_t tile_id, uint32_t ntx, const uint32_t tile_dim[2], 
  * (ConfigParser.cpp:79-97). */
 int cvr_scene_load(const char* path, int scene_type, cvr_scene** out);
 /* Synthetic proxies for the missing data blobs:
- * "bucky" (32^3 raw), "manix" (256x230x256 VDB-like), "hetvol" (128x128x50).
- * dims may be NULL (default size). */
+ * "bucky" (32^3 raw), "manix" (256x230x256 VDB-like), "hetvol" (128x128x50),
+ * "cloud" (C5: sparse fBm cumulus in a 2048x1024x2048 index box, albedo
+ * (1,1,1), stored sparse only).  dims may be NULL (default size). */
 int cvr_scene_synthetic(const char* name, uint32_t seed, const uint32_t* dims, cvr_scene** out);
 /* Medium description; pointers stay owned by the scene. */
 int cvr_scene_medium(const cvr_scene* scene, cvr_medium_desc* out);
+/* Sparse view of a scene: sparse scenes (the "cloud" proxy) are stored as
+ * leaves; a dense scene is converted once (leaves holding any non-zero
+ * density or an albedo other than the voxel (0,0,0)'s, which becomes the
+ * background) and the leaves are kept in the scene.  Pointers stay valid
+ * while the scene lives.  Dense scenes: cvr_scene_medium; a sparse scene has
+ * no dense view (CVR_ERR_UNSUPPORTED). */
+int cvr_scene_sparse_medium(cvr_scene* scene, cvr_sparse_medium_desc* out);
+/* 1 if the scene is stored sparse only. */
+int cvr_scene_is_sparse(const cvr_scene* scene);
 /* The scene's camera at a render resolution: the fixed eye and orientation
  * of Camera.h:25-45 with the scene's horizontal fov (0.7 degrees for VDB,
  * Raw and MHD scenes; the XML sensor's fov, default 45, for Mitsuba scenes,

@@ -97,6 +97,14 @@ typedef struct {
   float scale, max_density, g;
   float roughness[2];
   float eta; /* int_ior / ext_ior */
+  /* Optional 8^3-leaf storage of the same grid (cvr_sparse_medium_desc
+   * layout); when `leaves` is set, density/albedo are unused.  A storage
+   * format only: texel values are those of the densified grid. */
+  const uint32_t* leaves;
+  uint32_t leaf_dims[3];
+  const float* leaf_density;
+  const float* leaf_albedo; /* NULL: albedo_bg everywhere */
+  float albedo_bg[4];
 } oracle_medium;
 
 typedef struct {
@@ -133,6 +141,23 @@ static inline uint32_t texel(int i, uint32_t res) {
 /* lerp convention shared with the kernels: fma(b, f, a*(1-f)) */
 static inline float lerpf(float a, float b, float f, float fi) { return det_fmaf(b, f, a * fi); }
 
+static inline float tex_density(const oracle_medium* m, uint32_t x, uint32_t y, uint32_t z) {
+  if (m->leaves) {
+    uint32_t slot = m->leaves[((size_t)(z >> 3) * m->leaf_dims[1] + (y >> 3)) * m->leaf_dims[0] + (x >> 3)];
+    if (slot == 0xFFFFFFFFu) return 0.0f;
+    return m->leaf_density[(size_t)slot * 512 + ((z & 7) * 8 + (y & 7)) * 8 + (x & 7)];
+  }
+  return m->density[((size_t)z * m->res[1] + y) * m->res[0] + x];
+}
+static inline float tex_albedo(const oracle_medium* m, uint32_t x, uint32_t y, uint32_t z, int c) {
+  if (m->leaves) {
+    uint32_t slot = m->leaves[((size_t)(z >> 3) * m->leaf_dims[1] + (y >> 3)) * m->leaf_dims[0] + (x >> 3)];
+    if (slot == 0xFFFFFFFFu || !m->leaf_albedo) return m->albedo_bg[c];
+    return m->leaf_albedo[((size_t)slot * 512 + ((z & 7) * 8 + (y & 7)) * 8 + (x & 7)) * 4 + c];
+  }
+  return m->albedo[(((size_t)z * m->res[1] + y) * m->res[0] + x) * 4 + c];
+}
+
 typedef struct { int x1, y1, z1; float fx, fy, fz; } tri_t;
 static inline tri_t tri_setup(f3 p, const uint32_t res[3]) {
   /* DeviceVolume::volumeToGrid: p * (res - 1) */
@@ -154,8 +179,7 @@ static float density_lookup(const oracle_medium* m, f3 p) {
   uint32_t xa = texel(t.x1, rx), xb = texel(t.x1 + 1, rx);
   uint32_t ya = texel(t.y1, ry), yb = texel(t.y1 + 1, ry);
   uint32_t za = texel(t.z1, rz), zb = texel(t.z1 + 1, rz);
-  const float* D = m->density;
-#define DV(x, y, z) D[((size_t)(z) * ry + (y)) * rx + (x)]
+#define DV(x, y, z) tex_density(m, x, y, z)
   float d000 = DV(xa, ya, za), d001 = DV(xb, ya, za), d010 = DV(xa, yb, za), d011 = DV(xb, yb, za);
   float d100 = DV(xa, ya, zb), d101 = DV(xb, ya, zb), d110 = DV(xa, yb, zb), d111 = DV(xb, yb, zb);
 #undef DV
@@ -170,11 +194,10 @@ static f3 albedo_lookup(const oracle_medium* m, f3 p) {
   uint32_t xa = texel(t.x1, rx), xb = texel(t.x1 + 1, rx);
   uint32_t ya = texel(t.y1, ry), yb = texel(t.y1 + 1, ry);
   uint32_t za = texel(t.z1, rz), zb = texel(t.z1 + 1, rz);
-  const float* A = m->albedo;
   float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
   float out[3];
   for (int c = 0; c < 3; ++c) {
-#define AV(x, y, z) A[(((size_t)(z) * ry + (y)) * rx + (x)) * 4 + c]
+#define AV(x, y, z) tex_albedo(m, x, y, z, c)
     float d000 = AV(xa, ya, za), d001 = AV(xb, ya, za), d010 = AV(xa, yb, za), d011 = AV(xb, yb, za);
     float d100 = AV(xa, ya, zb), d101 = AV(xb, ya, zb), d110 = AV(xa, yb, zb), d111 = AV(xb, yb, zb);
 #undef AV

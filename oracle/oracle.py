@@ -24,7 +24,10 @@ class OracleMedium(C.Structure):
     _fields_ = [("res", C.c_uint32 * 3), ("density", C.POINTER(C.c_float)),
                 ("albedo", C.POINTER(C.c_float)), ("box_min", C.c_float * 3),
                 ("box_max", C.c_float * 3), ("scale", C.c_float), ("max_density", C.c_float),
-                ("g", C.c_float), ("roughness", C.c_float * 2), ("eta", C.c_float)]
+                ("g", C.c_float), ("roughness", C.c_float * 2), ("eta", C.c_float),
+                ("leaves", C.POINTER(C.c_uint32)), ("leaf_dims", C.c_uint32 * 3),
+                ("leaf_density", C.POINTER(C.c_float)), ("leaf_albedo", C.POINTER(C.c_float)),
+                ("albedo_bg", C.c_float * 4)]
 
 
 class OracleLaunch(C.Structure):
@@ -104,6 +107,29 @@ class Oracle:
         m.roughness[:] = roughness
         m.eta = np.float32(np.float32(1.05) / np.float32(1.01)) if eta is None else eta
         self.m = m
+
+    @classmethod
+    def from_leaves(cls, res, table, leaf_density, leaf_albedo, albedo_bg, box_min=(-0.5,) * 3,
+                    box_max=(0.5,) * 3, scale=100.0, max_density=1.0, g=0.0, roughness=(0.1, 0.1), eta=None):
+        """The same walk over 8^3-leaf storage (cvr_sparse_medium_desc layout):
+        `table` (lz, ly, lx) u32 slots or 0xFFFFFFFF, `leaf_density` (n, 512),
+        `leaf_albedo` (n, 512, 4) or None (albedo_bg everywhere)."""
+        nx, ny, nz = (int(v) for v in res)
+        o = cls(np.zeros((1, 1, 1), np.float32), np.zeros((1, 1, 1, 4), np.float32), box_min, box_max, scale,
+                max_density, g, roughness, eta)
+        o.table = np.ascontiguousarray(table, np.uint32)
+        o.leaf_density = np.ascontiguousarray(leaf_density, np.float32)
+        o.leaf_albedo = None if leaf_albedo is None else np.ascontiguousarray(leaf_albedo, np.float32)
+        m = o.m
+        m.res[:] = (nx, ny, nz)
+        m.leaves = o.table.ctypes.data_as(C.POINTER(C.c_uint32))
+        lz, ly, lx = o.table.shape
+        m.leaf_dims[:] = (lx, ly, lz)
+        m.leaf_density = o.leaf_density.ctypes.data_as(C.POINTER(C.c_float))
+        if o.leaf_albedo is not None:
+            m.leaf_albedo = o.leaf_albedo.ctypes.data_as(C.POINTER(C.c_float))
+        m.albedo_bg[:] = tuple(albedo_bg)
+        return o
 
     @classmethod
     def from_medium_desc(cls, desc, density, albedo):
