@@ -26,6 +26,9 @@ for step in "$@"; do
     pytest) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q -x --timeout 900 -p no:cacheprovider ;;
     pytestall) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q --timeout 900 -p no:cacheprovider ;;
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
+    bench_c3) run bench_c3 600 python3 bench.py --steps 10 --warmup 2 --scene hetvol ;;
+    bench_c4) run bench_c4 600 python3 bench.py --steps 3 --warmup 1 --shard tiles --resolution 2048 2048 --iterations 256 --no-cpu-baseline ;;
+    bench_c5) run bench_c5 600 python3 bench.py --steps 5 --warmup 1 --scene cloud ;;
     prof) run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
