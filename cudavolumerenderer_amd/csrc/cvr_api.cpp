@@ -497,6 +497,9 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
     return set_err(&c->err, CVR_ERR_INVALID, "empty grid");
   const size_t n = (size_t)md->res[0] * md->res[1] * md->res[2];
   if (n > 0xFFFFFFFFull) return set_err(&c->err, CVR_ERR_INVALID, "grid exceeds 2^32 voxels");
+  // the kernels index cells and bricks with 24-bit multiplies
+  if ((uint64_t)md->res[1] * md->res[2] >= (1ull << 24) || (uint64_t)md->res[0] * md->res[1] >= (1ull << 24))
+    return set_err(&c->err, CVR_ERR_UNSUPPORTED, "dense grid with y*z or x*y >= 2^24: use cvr_set_medium_sparse");
   int r = ensure_device(c);
   if (r) return r;
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -539,6 +542,7 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   m.bshift = c->bound_shift;
   m.bnx = bnx;
   m.bny = bny;
+  m.bnxy = bnx * bny;
   m.cells = c->d_cells;
   m.density = c->d_density;
   m.albedo = c->d_albedo;
@@ -627,6 +631,9 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
   m.bny = (res[1] + B - 1) / B;
   const uint32_t bnz = (res[2] + B - 1) / B;
   const size_t nb = (size_t)m.bnx * m.bny * bnz;
+  m.bnxy = m.bnx * m.bny;
+  if ((uint64_t)m.bnx * m.bny >= (1ull << 24) || nb > 0xFFFFFFFFull)
+    return set_err(&c->err, CVR_ERR_UNSUPPORTED, "sparse grid has too many bricks (%zu)", nb);
   HIP_TRY(c, hipMalloc(&c->d_sbounds, nb * sizeof(uint32_t)));
   if (c->use_cells) HIP_TRY(c, hipMalloc(&c->d_cells, ncl * 1024 * sizeof(float4)));
   uint32_t *d_coords = nullptr, *d_slot = nullptr;

@@ -88,6 +88,7 @@ struct MediumParams {
   // May be null (every point is fetched).
   const uint8_t* __restrict__ bounds;
   uint32_t bshift, bnx, bny;  // brick size log2, bricks per x / y row
+  uint32_t bnxy;              // bnx * bny (< 2^24)
   float bq;                   // (1/254)(1 + 2^-16): q -> bound on rho*inv_sigma
   // Sparse storage (cvr_set_medium_sparse; all null for a dense medium):
   // 8^3-voxel leaves, slot = leaves[leaf index] or CVR_NO_LEAF (density 0,
@@ -302,16 +303,19 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 // q*bq: when q*bq < xi the point is a null collision whatever rho is, and the
 // cell is not fetched.  Points whose lower corner lies outside the grid
 // (quirk Q5 taps, NaN) use q = 255 (never bounded out) and the 8-tap gather.
-CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
-                          uint32_t& n_steps, uint32_t& n_density, uint32_t& n_fetch) {
+//
+// Result: 0 null collision (continue), 1 t > max_t (no density evaluation),
+// 2 real collision with t < max_t, 3 real collision at t == max_t (the
+// reference scatters iff t < max_t, so this ends the segment at the box).
+// Every step but a 1 evaluates the density once.
+CVR_DEV int woodcock_step_core(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
+                               uint32_t& n_fetch) {
   const float xi = rng_float(rng);
   // == det_logf(det_fmaxf(xi, EPSILON)): xi is never NaN and the clamped
   // argument is a normal float, so the NaN and subnormal paths are dropped.
   t = det_fmaf(-det_logf_normal(xi < CVR_EPSILON_F ? CVR_EPSILON_F : xi), m.inv_sigma, t);
-  ++n_steps;
   if (!(t <= max_t)) return 1;
   const V3 c = sub3(mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z)), m.shift);
-  ++n_density;
   const float xi_test = rng_float(rng);
   // cell of the tentative point (DeviceVolume::volumeToGrid + floor)
   const float cx = c.x * m.gx, cy = c.y * m.gy, cz = c.z * m.gz;
@@ -320,18 +324,23 @@ CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float&
   const bool in = (fx1 >= 0.0f) & (fx1 < m.fres_x) & (fy1 >= 0.0f) & (fy1 < m.fres_y) & (fz1 >= 0.0f) &
                   (fz1 < m.fres_z);
   const uint32_t x1 = in ? (uint32_t)fx1 : 0u, y1 = in ? (uint32_t)fy1 : 0u, z1 = in ? (uint32_t)fz1 : 0u;
-  const uint32_t bi = (__umul24(z1 >> m.bshift, m.bny) + (y1 >> m.bshift)) * m.bnx + (x1 >> m.bshift);
+  // 24-bit multiplies: the host keeps bnx*bny, rx*ry and ry*rz below 2^24
+  const uint32_t bi = __umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift);
   const float4* cp;
+  // x1 = y1 = z1 = 0 when !in, so bi is a valid index either way: the bound
+  // is loaded unconditionally and replaced afterwards (no branch)
   if (m.sbounds) {  // sparse: bound and cell-leaf slot in one word
-    const uint32_t e = in ? m.sbounds[bi] : 0xFF000000u;
+    const uint32_t sw = m.sbounds[bi];
+    const uint32_t e = in ? sw : 0xFF000000u;
     if ((float)(e >> 24) * m.bq < xi_test) return 0;
     cp = m.cells + ((((size_t)(e & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
   } else {
     if (m.bounds) {
-      const uint32_t q = in ? (uint32_t)m.bounds[bi] : 255u;
+      const uint32_t qb = m.bounds[bi];
+      const uint32_t q = in ? qb : 255u;
       if ((float)q * m.bq < xi_test) return 0;
     }
-    cp = m.cells + 2 * ((__umul24(z1, m.ry) + y1) * m.rx + x1);
+    cp = m.cells + 2 * (__umul24(__umul24(z1, m.ry) + y1, m.rx) + x1);
   }
   ++n_fetch;
   float dens;
@@ -342,8 +351,17 @@ CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float&
     dens = density_lookup_gather(m, c);
   }
   const float rho = m.scale * dens;
-  if (!(rho * m.inv_sigma < xi_test)) return 2;
+  if (!(rho * m.inv_sigma < xi_test)) return t < max_t ? 2 : 3;
   return 0;
+}
+// Per-lane counting wrapper: 0 continue, 1 t > max_t, 2 real collision
+// (the caller scatters iff also t < max_t).
+CVR_DEV int woodcock_step(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
+                          uint32_t& n_steps, uint32_t& n_density, uint32_t& n_fetch) {
+  ++n_steps;
+  const int r = woodcock_step_core(m, o, d, max_t, t, rng, n_fetch);
+  n_density += r != 1;
+  return r == 3 ? 2 : r;
 }
 
 // --------------------------------------------------------------- HG -------

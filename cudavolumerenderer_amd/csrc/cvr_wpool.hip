@@ -164,6 +164,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   __syncthreads();
   uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint32_t seg_sum = 0;
+  uint32_t n_over = 0;  // wave-uniform: segments whose last Woodcock step passed max_t
   Cursor cur{0, 0, 0, (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % L.n_queues, false};
   const uint32_t batch = L.batch;  // TRACK: swap finished segments once this many lanes are idle
   // wave-uniform list state
@@ -192,25 +193,28 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     // before the event code runs, so nothing of it is live across that code
     // (keeps the step loop free of spills).
     int slot = -1;      // pool slot of the lane's path, -1 = none
-    bool fin = false;   // the segment ended; filed at the next swap
-    bool coll = false;  // ... as a real collision (else a boundary)
+    // woodcock_step_core result of the lane's segment: 0 still tracking,
+    // 2 real collision, 1/3 boundary (1: the last step evaluated no
+    // density); filed at the next swap
+    int fst = 0;
     V3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
     Rng rng{0, 0, 0, 0, 0, 0};
     float t = 0.0f, max_t = 0.0f;
     for (;;) {
-      const unsigned long long trk = __ballot(slot >= 0 && !fin);
+      const unsigned long long trk = __ballot(slot >= 0 && fst == 0);
       const uint32_t n_trk = (uint32_t)__popcll(trk);
       // ---- swap: file finished segments, pull track-ready paths ----------
       if (64u - n_trk >= batch || n_trk == 0u) {
-        if (fin) store_track(S, (uint32_t)slot, t, rng);
-        const unsigned long long mc = __ballot(fin && coll), mb = __ballot(fin && !coll);
-        if (fin && coll) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
-        if (fin && !coll) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
+        if (fst != 0) store_track(S, (uint32_t)slot, t, rng);
+        const unsigned long long mc = __ballot(fst == 2), mb = __ballot(fst & 1);
+        if (fst == 2) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
+        if (fst & 1) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
         n_lc += (uint32_t)__popcll(mc);
         n_lb += (uint32_t)__popcll(mb);
-        if (fin) {
+        n_over += (uint32_t)__popcll(__ballot(fst == 1));
+        if (fst != 0) {
           slot = -1;
-          fin = false;
+          fst = 0;
         }
         const unsigned long long idle = __ballot(slot < 0);
         const uint32_t k = min((uint32_t)__popcll(idle), n_ready), rank = lane_rank(idle);
@@ -228,18 +232,19 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
         n_ready -= k;
       }
-      const uint32_t n_act = (uint32_t)__popcll(__ballot(slot >= 0 && !fin));
-      const uint32_t n_fin = (uint32_t)__popcll(__ballot(fin));
+      const uint32_t n_act = (uint32_t)__popcll(__ballot(slot >= 0 && fst == 0));
+      const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0));
       // EVENT next: a full wave of waiting events, slots never filled, or
       // nothing left to track.  Park: tracking lanes return (t, rng) to the
       // pool, finished lanes are filed.
       if (n_lb + n_lc + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
         if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
-        const unsigned long long mr = __ballot(slot >= 0 && !fin);
-        const unsigned long long mc = __ballot(fin && coll), mb = __ballot(fin && !coll);
-        if (slot >= 0 && !fin) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)slot;
-        if (fin && coll) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
-        if (fin && !coll) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
+        const unsigned long long mr = __ballot(slot >= 0 && fst == 0);
+        const unsigned long long mc = __ballot(fst == 2), mb = __ballot(fst & 1);
+        if (slot >= 0 && fst == 0) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)slot;
+        if (fst == 2) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
+        if (fst & 1) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
+        n_over += (uint32_t)__popcll(__ballot(fst == 1));
         n_ready += (uint32_t)__popcll(mr);
         n_lc += (uint32_t)__popcll(mc);
         n_lb += (uint32_t)__popcll(mb);
@@ -251,12 +256,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
 #pragma unroll
       for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
-        if (slot >= 0 && !fin) {
-          const int r = woodcock_step(m, o, d, max_t, t, rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
-          if (r != 0) {
-            fin = true;
-            coll = (r == 2) && (t < max_t);
-          }
+        // density evaluations are steps minus the segments that ended past
+        // max_t (counted when filed), so only steps are counted here
+        if (slot >= 0 && fst == 0) {
+          ++c[STAT_STEPS];
+          fst = woodcock_step_core(m, o, d, max_t, t, rng, c[STAT_FETCH]);
         }
       }
     }
@@ -438,11 +442,13 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
   // ---- counters ------------------------------------------------------------
   c[STAT_SEGMENTS] = seg_sum;
+  c[STAT_DENSITY] = c[STAT_STEPS];
 #pragma unroll
   for (int k = 0; k < STAT_COUNT; ++k) {
     unsigned long long v = c[k];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    if (k == STAT_DENSITY) v -= n_over;  // wave totals: steps minus segments ended past max_t
     if (lane == 0 && v) atomicAdd(L.stats + k, v);
   }
 #if CVR_STAMPS
