@@ -65,6 +65,27 @@ CVR_DEV uint32_t rng_next(Rng& s) {
   s.d += 362437u;
   return s.v4 + s.d;
 }
+// Inverse of rng_next's state transition (takes back the last draw).  The
+// new word is n = (v4 ^ (v4 << 4)) ^ (u ^ (u << 1)) with u = v0 ^ (v0 >> 2);
+// both xorshifts are invertible by prefix xors.
+CVR_DEV void rng_undo(Rng& s) {
+  uint32_t u = s.v4 ^ s.v3 ^ (s.v3 << 4);  // = u ^ (u << 1)
+  u ^= u << 1;
+  u ^= u << 2;
+  u ^= u << 4;
+  u ^= u << 8;
+  u ^= u << 16;  // u
+  u ^= u >> 2;
+  u ^= u >> 4;
+  u ^= u >> 8;
+  u ^= u >> 16;  // v0
+  s.v4 = s.v3;
+  s.v3 = s.v2;
+  s.v2 = s.v1;
+  s.v1 = s.v0;
+  s.v0 = u;
+  s.d -= 362437u;
+}
 CVR_DEV float rng_float(Rng& s) {
   return det_fmaf((float)rng_next(s), 2.3283064e-10f, 1.1641532e-10f);
 }
@@ -308,49 +329,73 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 // 2 real collision with t < max_t, 3 real collision at t == max_t (the
 // reference scatters iff t < max_t, so this ends the segment at the box).
 // Every step but a 1 evaluates the density once.
-CVR_DEV int woodcock_step_core(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
-                               uint32_t& n_fetch) {
-  const float xi = rng_float(rng);
-  // == det_logf(det_fmaxf(xi, EPSILON)): xi is never NaN and the clamped
-  // argument is a normal float, so the NaN and subnormal paths are dropped.
-  t = det_fmaf(-det_logf_normal(xi < CVR_EPSILON_F ? CVR_EPSILON_F : xi), m.inv_sigma, t);
-  if (!(t <= max_t)) return 1;
-  const V3 c = sub3(mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z)), m.shift);
-  const float xi_test = rng_float(rng);
-  // cell of the tentative point (DeviceVolume::volumeToGrid + floor)
-  const float cx = c.x * m.gx, cy = c.y * m.gy, cz = c.z * m.gz;
-  const float fx1 = __builtin_floorf(cx), fy1 = __builtin_floorf(cy), fz1 = __builtin_floorf(cz);
+// Tentative point of a Woodcock step: its cell, brick bound and cell pointer.
+struct WoodcockPoint {
+  V3 c;                 // worldToAABB coordinate (Q4)
+  float cx, cy, cz;     // grid coordinate (DeviceVolume::volumeToGrid)
+  float fx1, fy1, fz1;  // floor
+  bool in;              // lower corner inside the grid (cell path), else the 8-tap gather
+  float qb;             // brick bound as q*bq (255*bq: no bound)
+  const float4* cp;     // the cell's two float4 (valid when in && m.cells)
+};
+CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t) {
+  WoodcockPoint P;
+  P.c = sub3(mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z)), m.shift);
+  P.cx = P.c.x * m.gx;
+  P.cy = P.c.y * m.gy;
+  P.cz = P.c.z * m.gz;
+  P.fx1 = __builtin_floorf(P.cx);
+  P.fy1 = __builtin_floorf(P.cy);
+  P.fz1 = __builtin_floorf(P.cz);
   // bitwise &: one mask, no short-circuit branches; NaN fails every compare
-  const bool in = (fx1 >= 0.0f) & (fx1 < m.fres_x) & (fy1 >= 0.0f) & (fy1 < m.fres_y) & (fz1 >= 0.0f) &
-                  (fz1 < m.fres_z);
-  const uint32_t x1 = in ? (uint32_t)fx1 : 0u, y1 = in ? (uint32_t)fy1 : 0u, z1 = in ? (uint32_t)fz1 : 0u;
+  P.in = (P.fx1 >= 0.0f) & (P.fx1 < m.fres_x) & (P.fy1 >= 0.0f) & (P.fy1 < m.fres_y) & (P.fz1 >= 0.0f) &
+         (P.fz1 < m.fres_z);
+  const uint32_t x1 = P.in ? (uint32_t)P.fx1 : 0u, y1 = P.in ? (uint32_t)P.fy1 : 0u,
+                 z1 = P.in ? (uint32_t)P.fz1 : 0u;
   // 24-bit multiplies: the host keeps bnx*bny, rx*ry and ry*rz below 2^24
   const uint32_t bi = __umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift);
-  const float4* cp;
   // x1 = y1 = z1 = 0 when !in, so bi is a valid index either way: the bound
   // is loaded unconditionally and replaced afterwards (no branch)
   if (m.sbounds) {  // sparse: bound and cell-leaf slot in one word
     const uint32_t sw = m.sbounds[bi];
-    const uint32_t e = in ? sw : 0xFF000000u;
-    if ((float)(e >> 24) * m.bq < xi_test) return 0;
-    cp = m.cells + ((((size_t)(e & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
+    const uint32_t e = P.in ? sw : 0xFF000000u;
+    P.qb = (float)(e >> 24) * m.bq;
+    P.cp = m.cells + ((((size_t)(e & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
   } else {
+    uint32_t q = 255u;
     if (m.bounds) {
       const uint32_t qb = m.bounds[bi];
-      const uint32_t q = in ? qb : 255u;
-      if ((float)q * m.bq < xi_test) return 0;
+      q = P.in ? qb : 255u;
     }
-    cp = m.cells + 2 * (__umul24(__umul24(z1, m.ry) + y1, m.rx) + x1);
+    P.qb = (float)q * m.bq;
+    P.cp = m.cells + 2 * (__umul24(__umul24(z1, m.ry) + y1, m.rx) + x1);
   }
+  return P;
+}
+// The exact density at the point (cell trilinear or the 8-tap gather).
+CVR_DEV float woodcock_density(const MediumParams& m, const WoodcockPoint& P) {
+  if (P.in && m.cells) {
+    const float4 lo = P.cp[0], hi = P.cp[1];
+    return trilerp8(lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, P.cx - P.fx1, P.cy - P.fy1, P.cz - P.fz1);
+  }
+  return density_lookup_gather(m, P.c);
+}
+// == det_logf(det_fmaxf(xi, EPSILON)) * -inv_sigma + t: xi is never NaN and
+// the clamped argument is a normal float, so the NaN and subnormal paths are
+// dropped.
+CVR_DEV float woodcock_advance(const MediumParams& m, float xi, float t) {
+  return det_fmaf(-det_logf_normal(xi < CVR_EPSILON_F ? CVR_EPSILON_F : xi), m.inv_sigma, t);
+}
+
+CVR_DEV int woodcock_step_core(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
+                               uint32_t& n_fetch) {
+  t = woodcock_advance(m, rng_float(rng), t);
+  if (!(t <= max_t)) return 1;
+  const WoodcockPoint P = woodcock_point(m, o, d, t);
+  const float xi_test = rng_float(rng);
+  if (P.qb < xi_test) return 0;  // bounded out (brick bound)
   ++n_fetch;
-  float dens;
-  if (in && m.cells) {
-    const float4 lo = cp[0], hi = cp[1];
-    dens = trilerp8(lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w, cx - fx1, cy - fy1, cz - fz1);
-  } else {
-    dens = density_lookup_gather(m, c);
-  }
-  const float rho = m.scale * dens;
+  const float rho = m.scale * woodcock_density(m, P);
   if (!(rho * m.inv_sigma < xi_test)) return t < max_t ? 2 : 3;
   return 0;
 }

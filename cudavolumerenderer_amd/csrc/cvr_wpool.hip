@@ -256,11 +256,27 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
 #pragma unroll
       for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
-        // density evaluations are steps minus the segments that ended past
-        // max_t (counted when filed), so only steps are counted here
+        // woodcock_step_core with both draws taken up front: a step that
+        // ends past max_t has drawn its test value too, and the boundary
+        // event takes that draw back (rng_undo).  With no draw inside a
+        // branch the RNG words need no per-path merge copies.  Density
+        // evaluations are steps minus the segments that ended past max_t
+        // (counted when filed), so only steps are counted here.
         if (slot >= 0 && fst == 0) {
           ++c[STAT_STEPS];
-          fst = woodcock_step_core(m, o, d, max_t, t, rng, c[STAT_FETCH]);
+          const float xi = rng_float(rng);
+          const float xt = rng_float(rng);
+          t = woodcock_advance(m, xi, t);
+          if (!(t <= max_t)) {
+            fst = 1;
+          } else {
+            const WoodcockPoint P = woodcock_point(m, o, d, t);
+            if (!(P.qb < xt)) {
+              ++c[STAT_FETCH];
+              const float rho = m.scale * woodcock_density(m, P);
+              if (!(rho * m.inv_sigma < xt)) fst = t < max_t ? 2 : 3;
+            }
+          }
         }
       }
     }
@@ -376,6 +392,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       CVR_LAP(9)
 #endif
       if (lane < tb + tc) load_full(S, s, ps, is, nseg, t_hit);
+      // a filed boundary whose last step passed max_t drew one number too many
+      if (lane < tb && !(t_hit <= is.dist)) rng_undo(ps.rng);
 #if CVR_STAMPS
       CVR_LAP(6)
 #endif
