@@ -471,6 +471,7 @@ static void fill_medium_common(cvr::MediumParams& m, const uint32_t res[3], cons
   m.rx = res[0];
   m.ry = res[1];
   m.rz = res[2];
+  m.rxy = res[0] * res[1];  // only used by dense media, where it is < 2^24
   m.fres_x = (float)res[0];
   m.fres_y = (float)res[1];
   m.fres_z = (float)res[2];

@@ -184,8 +184,9 @@ __global__ __launch_bounds__(256) void k_build_cells(const float* __restrict__ D
     const uint32_t x = (uint32_t)(i % rx), y = (uint32_t)((i / rx) % ry), z = (uint32_t)(i / ((size_t)rx * ry));
     const uint32_t xb = min(x + 1, rx - 1), yb = min(y + 1, ry - 1), zb = min(z + 1, rz - 1);
     auto at = [&](uint32_t a, uint32_t b, uint32_t c) { return D[((size_t)c * ry + b) * rx + a]; };
-    cells[2 * i] = make_float4(at(x, y, z), at(xb, y, z), at(x, yb, z), at(xb, yb, z));
-    cells[2 * i + 1] = make_float4(at(x, y, zb), at(xb, y, zb), at(x, yb, zb), at(xb, yb, zb));
+    // trilerp_cell layout: (d000, d100, d001, d101), (d010, d110, d011, d111), d{z}{y}{x}
+    cells[2 * i] = make_float4(at(x, y, z), at(x, y, zb), at(xb, y, z), at(xb, y, zb));
+    cells[2 * i + 1] = make_float4(at(x, yb, z), at(x, yb, zb), at(xb, yb, z), at(xb, yb, zb));
   }
 }
 
@@ -238,10 +239,10 @@ __global__ __launch_bounds__(256) void k_build_sparse_cells(MediumParams m, cons
       continue;
     }
     const uint32_t xb = min(x + 1, m.rx - 1), yb = min(y + 1, m.ry - 1), zb = min(z + 1, m.rz - 1);
-    cells[2 * i] = make_float4(texel_density(m, x, y, z), texel_density(m, xb, y, z), texel_density(m, x, yb, z),
-                               texel_density(m, xb, yb, z));
-    cells[2 * i + 1] = make_float4(texel_density(m, x, y, zb), texel_density(m, xb, y, zb),
-                                   texel_density(m, x, yb, zb), texel_density(m, xb, yb, zb));
+    cells[2 * i] = make_float4(texel_density(m, x, y, z), texel_density(m, x, y, zb), texel_density(m, xb, y, z),
+                               texel_density(m, xb, y, zb));
+    cells[2 * i + 1] = make_float4(texel_density(m, x, yb, z), texel_density(m, x, yb, zb),
+                                   texel_density(m, xb, yb, z), texel_density(m, xb, yb, zb));
   }
 }
 
