@@ -197,6 +197,18 @@ int ensure_output(cvr_ctx* c) {
   return CVR_OK;
 }
 
+// FastDiv constants for d >= 1 (cvr_walk.h fastdiv): l = ceil(log2 d),
+// m = floor(2^32 (2^l - d) / d) + 1, s1 = min(l, 1), s2 = max(l - 1, 0) (sh = s1 | s2 << 8).
+static cvr::FastDiv make_fastdiv(uint32_t d) {
+  if (d == 0) d = 1;
+  uint32_t l = 0;
+  while (l < 32 && (1ull << l) < d) ++l;
+  cvr::FastDiv f;
+  f.m = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+  f.sh = (l < 1 ? l : 1) | ((l > 1 ? l - 1 : 0) << 8);
+  return f;
+}
+
 void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_t count) {
   memcpy(L.M, c->inv_view, sizeof(L.M));
   L.r2v[0] = c->r2v[0];
@@ -238,6 +250,12 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
     L.n_blocks = 0;
     L.n_queues = 1;
   }
+  for (uint32_t q = 0; q <= 8; ++q)
+    L.qbeg[q] = q <= L.n_queues ? (uint32_t)((uint64_t)L.n_blocks * q / L.n_queues) : L.n_blocks;
+  L.div_tile_px = make_fastdiv(L.tile_px);
+  L.div_tile_w = make_fastdiv(L.tile_w);
+  L.div_block = make_fastdiv(64u * L.samples);
+  L.div_blocks_x = make_fastdiv(L.blocks_x);
 }
 
 int check_ready(cvr_ctx* c) {

@@ -136,6 +136,17 @@ struct MediumParams {
   float eta;         // int_ior / ext_ior
 };
 
+// u32 division by a launch-invariant divisor: q = (t + ((u - t) >> s1)) >> s2
+// with t = mulhi(u, m) (round-up method, exact for every u32 and d >= 1;
+// host side: cvr_api.cpp make_fastdiv).
+struct FastDiv {
+  uint32_t m, sh;  // sh = s1 | s2 << 8
+};
+CVR_DEV uint32_t fastdiv(uint32_t u, const FastDiv& f) {
+  const uint32_t t = __umulhi(u, f.m);
+  return (t + ((u - t) >> (f.sh & 0xFFu))) >> (f.sh >> 8);
+}
+
 struct LaunchParams {
   float M[12];            // c_inv_view_mat
   float r2v[2];           // c_raster_to_view
@@ -167,11 +178,13 @@ struct LaunchParams {
   uint32_t blocks_x;      // tile_w / 8
   uint32_t n_blocks;      // tile_px / 64
   uint32_t n_queues;      // 1..8
+  uint32_t qbeg[9];       // first block of each queue's band (order 1), qbeg[n_queues] = n_blocks
+  FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x;  // by tile_px, tile_w, 64*samples, blocks_x
 };
 
 // Map the u-th work unit of queue q to a path id (order 1), see LaunchParams.
 CVR_DEV uint32_t queue_blocks_begin(const LaunchParams& L, uint32_t q) {
-  return (uint32_t)(((unsigned long long)L.n_blocks * q) / L.n_queues);
+  return L.qbeg[q];  // n_blocks * q / n_queues
 }
 CVR_DEV uint32_t queue_units(const LaunchParams& L, uint32_t q) {
   if (L.order == 0) return q == 0 ? L.path_count : 0u;
@@ -180,10 +193,12 @@ CVR_DEV uint32_t queue_units(const LaunchParams& L, uint32_t q) {
 CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.order == 0) return L.path_first + u;
   const uint32_t per_block = 64u * L.samples;
-  const uint32_t b = queue_blocks_begin(L, q) + u / per_block;
-  const uint32_t rem = u % per_block;
+  const uint32_t bq = fastdiv(u, L.div_block);
+  const uint32_t b = queue_blocks_begin(L, q) + bq;
+  const uint32_t rem = u - bq * per_block;
   const uint32_t s = rem >> 6, lane = rem & 63u;
-  const uint32_t px = (b % L.blocks_x) * 8u + (lane & 7u), py = (b / L.blocks_x) * 8u + (lane >> 3);
+  const uint32_t by = fastdiv(b, L.div_blocks_x);
+  const uint32_t px = (b - by * L.blocks_x) * 8u + (lane & 7u), py = by * 8u + (lane >> 3);
   return L.path_first + s * L.tile_px + py * L.tile_w + px;
 }
 
@@ -606,9 +621,9 @@ struct PathState {
   uint32_t image_id;
 };
 CVR_DEV void path_begin(const LaunchParams& L, uint32_t path_id, PathState& ps) {
-  ps.image_id = path_id % L.tile_px;
+  ps.image_id = path_id - fastdiv(path_id, L.div_tile_px) * L.tile_px;  // path_id % tile_px
   rng_init(ps.rng, (int32_t)(L.seed_base + path_id));
-  const float px = (float)(ps.image_id % L.tile_w) + (float)L.off[0];
+  const float px = (float)(ps.image_id - fastdiv(ps.image_id, L.div_tile_w) * L.tile_w) + (float)L.off[0];
   const float py = det_floorf((float)ps.image_id / L.tile_res[0]) + (float)L.off[1];
   const float r0 = rng_float(ps.rng);
   const float r1 = rng_float(ps.rng);

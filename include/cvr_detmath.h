@@ -162,25 +162,20 @@ CVR_HD float det_asin_poly(float x, float z) { /* x + x^3 A(x^2), |x| <= 0.5 */
   a = det_fmaf(a, z, 0.16666659712791443f);
   return det_fmaf(x * z, a, x);
 }
+/* Three ranges, evaluated branch-free (one polynomial, selected inputs):
+ *   |x| <= 0.5: pi/2 - asin(x)
+ *   x > 0.5:    2 asin(sqrt((1 - x)/2))
+ *   x < -0.5:   2 (pi/2 - asin(sqrt((1 + x)/2)))
+ * (GGX lanes straddle the ranges, so branches would run all of them.) */
 CVR_HD float det_acosf(float x) {
   const float pio2_hi = 1.5707963705062866f, pio2_lo = -4.371138828673793e-08f;
-  if (!(x >= -1.0f && x <= 1.0f)) return __builtin_nanf("");
-  if (det_fabsf(x) <= 0.5f) {
-    float z = x * x;
-    float as = det_asin_poly(x, z);
-    return pio2_hi - (as - pio2_lo);
-  }
-  if (x > 0.0f) {
-    float z = (1.0f - x) * 0.5f;
-    float s = det_sqrtf(z);
-    return 2.0f * det_asin_poly(s, z);
-  }
-  {
-    float z = (1.0f + x) * 0.5f;
-    float s = det_sqrtf(z);
-    float as = det_asin_poly(s, z);
-    return 2.0f * (pio2_hi - (as - pio2_lo));
-  }
+  const int mid = det_fabsf(x) <= 0.5f;
+  const float zo = (x > 0.0f ? 1.0f - x : 1.0f + x) * 0.5f;
+  const float z = mid ? x * x : zo;
+  const float so = det_sqrtf(zo);
+  const float as = det_asin_poly(mid ? x : so, z);
+  const float r = mid ? pio2_hi - (as - pio2_lo) : (x > 0.0f ? 2.0f * as : 2.0f * (pio2_hi - (as - pio2_lo)));
+  return (x >= -1.0f && x <= 1.0f) ? r : __builtin_nanf("");
 }
 
 /* -------------------------------------------------------------- atan2 --- */
