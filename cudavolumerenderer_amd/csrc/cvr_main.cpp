@@ -7,7 +7,7 @@
 //       [--iterations|-i N] [--resolution|-r W [H]] [--number-of-tiles X [Y]]
 //       [--trials N] [--output|-o NAME] [--interactive BOOL]
 //       [--use-unified-memory BOOL]
-//   extensions: --synthetic bucky|manix|hetvol, --device N, --seed S
+//   extensions: --synthetic bucky|manix|hetvol|cloud, --device N, --seed S
 //
 // Differences from the reference, on purpose: the timer is wall clock (the
 // reference uses clock(), i.e. CPU time, Main.cpp:51-77); main does not wait
@@ -46,13 +46,13 @@ void usage() {
       "  -a [ --algorithm ] arg (=cudaVolPath)\n"
       "  -k [ --kernel ] arg (=regenerationSK)\n"
       "  --number-of-tiles arg (=1 1)\n"
-      "  --use-unified-memory arg (=0)      accepted for compatibility (288 GB HBM)\n"
+      "  --use-unified-memory arg (=0)      1: upload the grid as sparse 8^3 leaves\n"
       "Scene configuration override:\n"
       "  -i [ --iterations ] arg (=20)\n"
       "  -o [ --output ] arg\n"
       "  -r [ --resolution ] arg (=1024 1024)\n"
       "Extensions:\n"
-      "  --synthetic bucky|manix|hetvol     use a built-in proxy scene\n"
+      "  --synthetic bucky|manix|hetvol|cloud  use a built-in proxy scene\n"
       "  --device N, --seed S\n");
 }
 
@@ -155,8 +155,18 @@ int main(int argc, char** argv) {
   if (o.output.empty())  // Config::operator<< (Config.h:237-248)
     o.output = "algorithm_" + o.algorithm + "_kernel_" + o.kernel + "_iter_" + std::to_string(o.iterations);
 
+  // Medium upload: dense textures as the reference; the 8^3-leaf upload for
+  // sparse-only scenes, for --use-unified-memory true (the reference's
+  // HostDeviceMedium choice for scenes too big for device memory,
+  // Config.h:147-156), and when the dense grid is rejected as too large.
   cvr_medium_desc md;
-  cvr_scene_medium(scene, &md);
+  cvr_sparse_medium_desc sd;
+  bool sparse = cvr_scene_is_sparse(scene) || o.unified;
+  if (!sparse) cvr_scene_medium(scene, &md);
+  if (sparse && (r = cvr_scene_sparse_medium(scene, &sd)) != CVR_OK) {
+    fprintf(stderr, "Error: sparse view of the scene failed (%d)\n", r);
+    return 1;
+  }
   const unsigned W = o.resolution[0], H = o.resolution[1];
   float inv_view[12], r2v[2];
   cvr_scene_camera(scene, W, H, inv_view, r2v);  // default camera; XML scenes carry their fov
@@ -172,7 +182,13 @@ int main(int argc, char** argv) {
       return 1;
     }
     cvr_set_seed(ctx, o.seed);
-    if ((r = cvr_set_medium(ctx, &md)) || (r = cvr_set_camera(ctx, inv_view, r2v, full_res)) || (r = cvr_init(ctx))) {
+    if (!sparse && (r = cvr_set_medium(ctx, &md)) == CVR_ERR_UNSUPPORTED) {
+      printf("[Scene] dense grid rejected (%s); using the sparse leaf upload\n", cvr_last_error(ctx));
+      if ((r = cvr_scene_sparse_medium(scene, &sd)) != CVR_OK) return 1;
+      sparse = true;
+    }
+    if (sparse) r = cvr_set_medium_sparse(ctx, &sd);
+    if (r || (r = cvr_set_camera(ctx, inv_view, r2v, full_res)) || (r = cvr_init(ctx))) {
       fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
       return 1;
     }
