@@ -23,7 +23,7 @@ ERRORS = {-1: "CVR_ERR_INVALID", -2: "CVR_ERR_HIP", -3: "CVR_ERR_STATE", -4: "CV
 # Config::Kernel order (Config.h:87-95)
 KERNELS = ["naiveSK", "naiveMK", "regenerationSK", "streamingMK", "streamingSK", "sortingSK"]
 NAIVE_SK, NAIVE_MK, REGENERATION_SK, STREAMING_MK, STREAMING_SK, SORTING_SK = range(6)
-SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4}
+SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4, "VdbSparse": 5}
 
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12

@@ -40,7 +40,7 @@ void usage() {
       "Generic:\n"
       "  -h [ --help ]                      produce help message\n"
       "  -s [ --scene-file ] arg            scene file to parse\n"
-      "  --scene-type arg (=Auto)           Auto, MitsubaXml, Vdb, Raw, Mhd\n"
+      "  --scene-type arg (=Auto)           Auto, MitsubaXml, Vdb, Raw, Mhd (+ VdbSparse)\n"
       "  --interactive arg (=1)             (no GL viewer in this build: runs headless)\n"
       "  --trials arg (=1)                  number of times to run the algorithm\n"
       "  -a [ --algorithm ] arg (=cudaVolPath)\n"
@@ -106,6 +106,7 @@ int scene_type_id(const std::string& t) {
   if (t == "Auto") return CVR_SCENE_AUTO;
   if (t == "MitsubaXml") return CVR_SCENE_MITSUBA_XML;
   if (t == "Vdb") return CVR_SCENE_VDB;
+  if (t == "VdbSparse") return CVR_SCENE_VDB_SPARSE;
   if (t == "Raw") return CVR_SCENE_RAW;
   if (t == "Mhd") return CVR_SCENE_MHD;
   return -1;

@@ -461,8 +461,8 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
       fclose(fp);
       r = (got == raw.size()) ? scene_from_raw_bytes(raw, p, s) : CVR_ERR_IO;  // Q16: report short files
     }
-  } else if (type == CVR_SCENE_VDB) {
-    r = load_vdb_scene(p, s);
+  } else if (type == CVR_SCENE_VDB || type == CVR_SCENE_VDB_SPARSE) {
+    r = load_vdb_scene(p, s, type == CVR_SCENE_VDB_SPARSE);
   } else if (type == CVR_SCENE_MHD) {
     r = load_mhd_scene(p, s);
   } else if (type == CVR_SCENE_MITSUBA_XML) {
@@ -472,7 +472,8 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
   }
   if (r != CVR_OK) {
     delete s;
-    if (type == CVR_SCENE_VDB && r == CVR_ERR_IO) set_last_error(std::string("VDB: ") + vdb_last_error());
+    if ((type == CVR_SCENE_VDB || type == CVR_SCENE_VDB_SPARSE) && r == CVR_ERR_IO)
+      set_last_error(std::string("VDB: ") + vdb_last_error());
     else if (type != CVR_SCENE_MITSUBA_XML)
       set_last_error("cannot load scene " + p + (r == CVR_ERR_UNSUPPORTED ? " (unsupported)" : ""));
     return r;

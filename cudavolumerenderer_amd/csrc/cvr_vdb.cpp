@@ -351,19 +351,22 @@ struct Tree {
     return any;
   }
 
-  // Densify like VDBAdapter::get*DataAsLinearArray: the ValueOn iterator
-  // visits every active leaf voxel and each active tile once, at the tile's
-  // origin (so a tile fills one voxel, not its extent: reference behaviour).
-  void densify(const int32_t lo[3], const uint32_t dim[3], float* out, int channels) const {
-    auto put = [&](int32_t x, int32_t y, int32_t z, const uint8_t* v) {
-      const size_t idx = (size_t)(x - lo[0]) + (size_t)dim[0] * ((size_t)(y - lo[1]) + (size_t)dim[1] * (size_t)(z - lo[2]));
-      memcpy(out + idx * (size_t)channels, v, VS);
-    };
+  // The ValueOn iterator of VDBAdapter::get*DataAsLinearArray: every active
+  // leaf voxel and each active tile once, at the tile's origin (so a tile
+  // fills one voxel, not its extent: reference behaviour).
+  template <class F>
+  void for_each_on(F&& put) const {
     for (const auto& lf : leaves)
       for (int i = 0; i < 512; ++i)
         if (lf.mask.on((size_t)i))
           put(lf.origin[0] + (i >> 6), lf.origin[1] + ((i >> 3) & 7), lf.origin[2] + (i & 7), lf.values.data() + (size_t)i * VS);
     for (const auto& t : active_tiles) put(t.origin[0], t.origin[1], t.origin[2], t.value.data());
+  }
+  void densify(const int32_t lo[3], const uint32_t dim[3], float* out, int channels) const {
+    for_each_on([&](int32_t x, int32_t y, int32_t z, const uint8_t* v) {
+      const size_t idx = (size_t)(x - lo[0]) + (size_t)dim[0] * ((size_t)(y - lo[1]) + (size_t)dim[1] * (size_t)(z - lo[2]));
+      memcpy(out + idx * (size_t)channels, v, VS);
+    });
   }
 };
 
@@ -414,7 +417,69 @@ int read_grid(const std::vector<uint8_t>& file, const GridDesc& gd, Tree<VS>& tr
 
 }  // namespace
 
-int load_vdb_scene(const std::string& path, cvr_scene* sc) {
+// Sparse read: the active values go straight into 8^3 leaves of the
+// density bounding box (the grid the dense path would build), without the
+// dense arrays.  Stored leaves are those holding a non-zero density or a
+// non-zero albedo; the rest read as density 0, albedo (0,0,0,1), which is
+// what densification leaves there.  The albedo must share the density box
+// (converter-made files do), so the reference's reinterpretation of the
+// albedo array with the density's dimensions is the identity.
+template <int VD, int VA>
+int vdb_to_leaves(const Tree<VD>& dt, const Tree<VA>& at, const int32_t lo[3], const uint32_t dim[3],
+                  cvr_scene* sc) {
+  const uint32_t lnx = (dim[0] + 7) / 8, lny = (dim[1] + 7) / 8, lnz = (dim[2] + 7) / 8;
+  const size_t nleaf = (size_t)lnx * lny * lnz;
+  if (nleaf > (1ull << 30)) return fail("density bounding box too large for the leaf table");
+  sc->leaf_dims[0] = lnx;
+  sc->leaf_dims[1] = lny;
+  sc->leaf_dims[2] = lnz;
+  sc->leaf_table.assign(nleaf, CVR_NO_LEAF);
+  sc->leaf_density.clear();
+  sc->leaf_albedo.clear();
+  auto slot_of = [&](uint32_t x, uint32_t y, uint32_t z) -> size_t {
+    uint32_t& e = sc->leaf_table[((size_t)(z >> 3) * lny + (y >> 3)) * lnx + (x >> 3)];
+    if (e == CVR_NO_LEAF) {
+      e = (uint32_t)(sc->leaf_density.size() / 512);
+      sc->leaf_density.resize(sc->leaf_density.size() + 512, 0.0f);
+      const size_t a = sc->leaf_albedo.size();
+      sc->leaf_albedo.resize(a + 2048, 0.0f);
+      for (size_t k = 3; k < 2048; k += 4) sc->leaf_albedo[a + k] = 1.0f;
+    }
+    return (size_t)e * 512 + (((z & 7) << 6) | ((y & 7) << 3) | (x & 7));
+  };
+  float mx = 0.0f;
+  dt.for_each_on([&](int32_t x, int32_t y, int32_t z, const uint8_t* v) {
+    float f;
+    memcpy(&f, v, 4);
+    mx = std::max(mx, f);
+    if (f != 0.0f) sc->leaf_density[slot_of(x - lo[0], y - lo[1], z - lo[2])] = f;
+  });
+  bool albedo_set = false;
+  at.for_each_on([&](int32_t x, int32_t y, int32_t z, const uint8_t* v) {
+    float c[3];
+    memcpy(c, v, 12);
+    if (c[0] == 0.0f && c[1] == 0.0f && c[2] == 0.0f) return;
+    const int32_t r[3] = {x - lo[0], y - lo[1], z - lo[2]};
+    if (r[0] < 0 || r[1] < 0 || r[2] < 0 || r[0] >= (int32_t)dim[0] || r[1] >= (int32_t)dim[1] || r[2] >= (int32_t)dim[2])
+      return;  // outside the density box: never read
+    memcpy(&sc->leaf_albedo[4 * slot_of(r[0], r[1], r[2])], c, 12);
+    albedo_set = true;
+  });
+  if (!albedo_set) std::vector<float>().swap(sc->leaf_albedo);
+  const float bg[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  memcpy(sc->albedo_bg, bg, sizeof(bg));
+  sc->sparse_only = true;
+  sc->have_leaves = true;
+  sc->max_density = mx;  // VDBSceneBuilder.h:54-77 (inactive voxels are 0)
+  sc->scale = 100.0f;
+  for (int k = 0; k < 3; ++k) {
+    sc->box_min[k] = -0.5f;
+    sc->box_max[k] = 0.5f;
+  }
+  return CVR_OK;
+}
+
+int load_vdb_scene(const std::string& path, cvr_scene* sc, bool sparse) {
   FILE* fp = fopen(path.c_str(), "rb");
   if (!fp) return fail("cannot open " + path);
   std::vector<uint8_t> file;
@@ -468,9 +533,16 @@ int load_vdb_scene(const std::string& path, cvr_scene* sc) {
   uint32_t dim[3], adim[3] = {0, 0, 0};
   for (int k = 0; k < 3; ++k) dim[k] = (uint32_t)(hi[k] - lo[k] + 1);
   const size_t n = (size_t)dim[0] * dim[1] * dim[2];
-  if (n > 0xFFFFFFFFull) return fail("density bounding box too large");
   sc->name = path;
   for (int k = 0; k < 3; ++k) sc->dims[k] = dim[k];
+  // more than 2^30 voxels (20 GB of dense host arrays): read sparse
+  if (sparse || n > (1ull << 30)) {
+    if (at.bbox(alo, ahi))
+      for (int k = 0; k < 3; ++k)
+        if (alo[k] != lo[k] || ahi[k] != hi[k])
+          return fail("sparse VDB read needs the albedo grid on the density grid's bounding box");
+    return vdb_to_leaves(dt, at, lo, dim, sc);
+  }
   sc->density.assign(n, 0.0f);  // inactive value 0
   dt.densify(lo, dim, sc->density.data(), 1);
   // Albedo: densified over the albedo grid's own bounding box, then read as

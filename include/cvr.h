@@ -53,7 +53,9 @@ typedef enum {
   CVR_SCENE_MITSUBA_XML = 1,
   CVR_SCENE_VDB = 2,
   CVR_SCENE_RAW = 3,
-  CVR_SCENE_MHD = 4
+  CVR_SCENE_MHD = 4,
+  CVR_SCENE_VDB_SPARSE = 5 /* extension: read a VDB straight into 8^3 leaves (cvr_scene_sparse_medium);
+                              Vdb/Auto do so by themselves above 2^30 voxels */
 } cvr_scene_type;
 
 /* Options for cvr_set_option. */

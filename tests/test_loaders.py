@@ -255,3 +255,63 @@ def test_xml_scene_errors(cvr, tmp_path):
     with pytest.raises(cvr.CvrError) as e:
         cvr.Scene.load(str(tmp_path / "bad.xml"))
     assert "gridvolume" in str(e.value)
+
+
+# ------------------------------------------------------ sparse VDB read ----
+def _densify_leaves(s):
+    table, dens, alb, bg = s.leaves()
+    nx, ny, nz = s.dims
+    lz, ly, lx = table.shape
+    D = np.zeros((lz * 8, ly * 8, lx * 8), np.float32)
+    A = np.empty((lz * 8, ly * 8, lx * 8, 4), np.float32)
+    A[:] = np.asarray(bg, np.float32)
+    for z, y, x in zip(*np.nonzero(table != 0xFFFFFFFF)):
+        k = table[z, y, x]
+        D[z * 8:z * 8 + 8, y * 8:y * 8 + 8, x * 8:x * 8 + 8] = dens[k]
+        if alb is not None:
+            A[z * 8:z * 8 + 8, y * 8:y * 8 + 8, x * 8:x * 8 + 8] = alb[k]
+    return D[:nz, :ny, :nx], A[:nz, :ny, :nx]
+
+
+@pytest.mark.parametrize("which", ["bonsai", "generated"])
+def test_vdb_sparse_read_equals_dense_read(cvr, tmp_path, which):
+    """VdbSparse reads the active values straight into 8^3 leaves; densified,
+    they are bit-identical to the dense read (density, albedo, majorant)."""
+    path = BONSAI
+    if which == "generated":
+        rng = np.random.default_rng(3)
+        nodes = _sparse_scene(rng)
+        nodes3 = {"leaves": [(o, m, np.stack([v, v * 0.5, v * 0.25], -1)) for (o, m, v) in nodes["leaves"]],
+                  "tiles16": [(o, (val, val * 0.5, val * 0.25)) for (o, val) in nodes["tiles16"]], "tiles32": []}
+        path = str(tmp_path / "gen.vdb")
+        write_vdb(path, {"density": (nodes, 1), "albedo": (nodes3, 3)}, "zip")
+    dense = cvr.Scene.load(path, "Vdb")
+    sparse = cvr.Scene.load(path, "VdbSparse")
+    assert sparse.is_sparse and sparse.dims == dense.dims
+    D, A = _densify_leaves(sparse)
+    assert np.array_equal(D.view(np.uint32), dense.density.view(np.uint32))
+    assert np.array_equal(A.view(np.uint32), dense.albedo.view(np.uint32))
+    assert sparse.max_density == dense.max_density
+    table, dens, _, _ = sparse.leaves()
+    assert (dens.reshape(len(dens), -1) != 0).any(axis=1).all() or which == "generated"
+
+
+def test_vdb_reader_goes_sparse_above_2pow30_voxels(cvr, tmp_path):
+    """A VDB whose active box exceeds 2^30 voxels (20 GB of dense host arrays)
+    is read into leaves by the plain Vdb/Auto types (C5-sized files)."""
+    rng = np.random.default_rng(5)
+    m = rng.uniform(size=512) < 0.5
+    v = np.where(m, rng.uniform(0.1, 1.0, 512), 0.0).astype(np.float32)
+    nodes = {"leaves": [((0, 0, 0), m, v), ((4088, 2040, 2040), m, v * 0.5)], "tiles16": [], "tiles32": []}
+    nodes3 = {"leaves": [(o, mm, np.stack([vv, vv, vv], -1)) for (o, mm, vv) in nodes["leaves"]],
+              "tiles16": [], "tiles32": []}
+    p = str(tmp_path / "huge.vdb")
+    write_vdb(p, {"density": (nodes, 1), "albedo": (nodes3, 3)}, "raw")
+    s = cvr.Scene.load(p)
+    assert s.is_sparse and s.dims == (4096, 2048, 2048)
+    table, dens, alb, bg = s.leaves()
+    assert table.shape == (256, 256, 512) and len(dens) == 2 and bg == (0.0, 0.0, 0.0, 1.0)
+    vx = v.reshape(8, 8, 8)  # VDB leaf index (x << 6) | (y << 3) | z -> [x, y, z]
+    assert np.array_equal(dens[table[0, 0, 0]], vx.transpose(2, 1, 0))
+    assert np.array_equal(dens[table[255, 255, 511]], (vx * np.float32(0.5)).transpose(2, 1, 0))
+    assert s.max_density == float(v.max())
