@@ -33,7 +33,7 @@
 #endif
 // Woodcock steps per track iteration between swap/event checks.
 #ifndef CVR_WPOOL_UNROLL
-#define CVR_WPOOL_UNROLL 3
+#define CVR_WPOOL_UNROLL 4
 #endif
 
 namespace cvr {
