@@ -541,8 +541,9 @@ CVR_DEV V3 ggx_sample_vndf(V3 wi_, float ax, float ay, float sx, float sy) {
 }
 // GGX.h:213-255
 CVR_DEV float project_roughness(V3 v, float ax, float ay) {
+  if (ax == ay) return ax;  // isotropic (the reference's 0.1, 0.1): no division needed
   const float invSinTheta2 = 1.0f / (1.0f - v.z * v.z);
-  if (ax == ay || invSinTheta2 <= 0.0f) return ax;
+  if (invSinTheta2 <= 0.0f) return ax;
   const float cosPhi2 = v.x * v.x * invSinTheta2;
   const float sinPhi2 = v.y * v.y * invSinTheta2;
   return det_sqrtf(cosPhi2 * ax * ax + sinPhi2 * ay * ay);
@@ -564,7 +565,11 @@ CVR_DEV bool ggx_sample(const MediumParams& m, V3 wi, Rng& rng, V3& wo, float& w
     return false;
   }
   weight = 1.0f;
-  const float sign = wi.z / det_fabsf(wi.z);
+  // wi.z / |wi.z| is +-1 exactly for a finite wi.z (!= 0 here); the
+  // division itself runs only for inf/NaN (same NaN as before)
+  float sign;
+  if (det_fabsf(wi.z) <= 3.40282347e38f) sign = wi.z > 0.0f ? 1.0f : -1.0f;
+  else sign = wi.z / det_fabsf(wi.z);
   const float s0 = rng_float(rng);
   const float s1 = rng_float(rng);
   const V3 wh = ggx_sample_vndf(scl3(wi, sign), m.ax, m.ay, s0, s1);
@@ -599,11 +604,19 @@ CVR_DEV bool ggx_sample(const MediumParams& m, V3 wi, Rng& rng, V3& wo, float& w
 struct Frame {
   V3 x, y, z;
 };
+// normalize3(v) is v itself, bit for bit, when dot(v, v) == 1 exactly
+// (sqrt(1) = 1, 1/1 = 1, v*1 = v): the AABB normals and their cross
+// products with the frame's helper axis take this branch and skip the
+// square root and the division.
+CVR_DEV V3 normalize3_unit_fast(V3 v) {
+  if (dot3(v, v) == 1.0f) return v;
+  return normalize3(v);
+}
 CVR_DEV Frame frame_from_z(V3 n) {
   Frame f;
-  f.z = normalize3(n);
+  f.z = normalize3_unit_fast(n);
   const V3 tx = (det_fabsf(f.z.x) > 0.99f) ? mk3(0, 1, 0) : mk3(1, 0, 0);
-  f.y = normalize3(cross3(f.z, tx));
+  f.y = normalize3_unit_fast(cross3(f.z, tx));
   f.x = cross3(f.y, f.z);
   return f;
 }
