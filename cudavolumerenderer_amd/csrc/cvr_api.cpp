@@ -506,6 +506,7 @@ static void fill_medium_common(cvr::MediumParams& m, const uint32_t res[3], cons
   m.ax = roughness[0];
   m.ay = roughness[1];
   m.eta = eta;
+  m.inv_eta = 1.0f / eta;
   m.bq = (float)((1.0 / 254.0) * (1.0 + 1.0 / 65536.0));
 }
 

@@ -134,6 +134,7 @@ struct MediumParams {
   float g;           // HG asymmetry (0 in the reference, Q7)
   float ax, ay;      // GGX roughness
   float eta;         // int_ior / ext_ior
+  float inv_eta;     // 1.0f / eta
 };
 
 // u32 division by a launch-invariant divisor: q = (t + ((u - t) >> s1)) >> s2
@@ -462,12 +463,12 @@ CVR_DEV V3 hg_sample(V3 v, float g, float e1, float e2) {
 
 // -------------------------------------------------------------- GGX -------
 // GGX.h:13-38
-CVR_DEV float fresnel_dielectric(float eta, float ndotwi, float& ndotwt) {
+CVR_DEV float fresnel_dielectric(float eta, float inv_eta, float ndotwi, float& ndotwt) {
   if (eta == 1.0f) {
     ndotwt = -ndotwi;
     return 0.0f;
   }
-  const float scale = (ndotwi > 0.0f) ? 1.0f / eta : eta;
+  const float scale = (ndotwi > 0.0f) ? inv_eta : eta;  // inv_eta = 1.0f / eta (host, same IEEE quotient)
   const float sin_sqr = 1.0f - ndotwi * ndotwi;
   const float ndotwt_sqr = 1.0f - (sin_sqr * scale) * scale;
   if (ndotwt_sqr <= 0.0f) {
@@ -575,7 +576,7 @@ CVR_DEV bool ggx_sample(const MediumParams& m, V3 wi, Rng& rng, V3& wo, float& w
   const V3 wh = ggx_sample_vndf(scl3(wi, sign), m.ax, m.ay, s0, s1);
   float whdotwt = __builtin_nanf("");
   const float whdotwi = dot3(wh, wi);
-  const float F = fresnel_dielectric(m.eta, whdotwi, whdotwt);
+  const float F = fresnel_dielectric(m.eta, m.inv_eta, whdotwi, whdotwt);
   if (rng_float(rng) <= F) {
     wo = sub3(scl3(wh, 2.0f * whdotwi), wi);
     if (wi.z * wo.z <= 0.0f) {
@@ -588,7 +589,7 @@ CVR_DEV bool ggx_sample(const MediumParams& m, V3 wi, Rng& rng, V3& wo, float& w
       return false;
     }
     float eta = m.eta;
-    if (whdotwt < 0.0f) eta = 1.0f / eta;
+    if (whdotwt < 0.0f) eta = m.inv_eta;
     wo = sub3(scl3(wh, whdotwi * eta + whdotwt), scl3(wi, eta));
     if (wi.z * wo.z >= 0.0f) {
       weight = 0.0f;
