@@ -47,24 +47,30 @@ template <int kWaves>
 struct PoolSize;
 template <>
 struct PoolSize<3> {
-  static constexpr int value = 166;
+  static constexpr int value = 159;
 };
 template <>
 struct PoolSize<4> {
-  static constexpr int value = 125;
+  static constexpr int value = 119;
 };
 template <>
 struct PoolSize<5> {
-  static constexpr int value = 96;
+  static constexpr int value = 94;
 };
 
+// One path per slot, array-of-structs in 16-byte blocks so a path moves with
+// ds_read_b128 / ds_write_b128 (5 per full path instead of 19 dword ops):
+//   a = (o.x, o.y, o.z, t)   b = (d.x, d.y, d.z, dist)   c = rng v0..v3
+//   e = (rng v4, rng d, image_id, meta)   f = (T.x, T.y, T.z, -)
+// meta: bits 0-2 normal code, bit 3 inside, bits 4.. segments so far.
+struct alignas(16) PoolSlot {
+  float4 a, b;
+  uint4 c, e;
+  float4 f;
+};
 template <int kSlots>
 struct WavePool {
-  float ox[kSlots], oy[kSlots], oz[kSlots], dx[kSlots], dy[kSlots], dz[kSlots];
-  float tx[kSlots], ty[kSlots], tz[kSlots], dist[kSlots], t[kSlots];
-  uint32_t r0[kSlots], r1[kSlots], r2[kSlots], r3[kSlots], r4[kSlots], rd[kSlots];
-  uint32_t img[kSlots];
-  uint32_t meta[kSlots];   // bits 0-2 normal code, bit 3 inside, bits 4.. segments so far
+  PoolSlot p[kSlots];
   uint8_t ready[kSlots];   // ring of track-ready slots
   uint8_t lb[kSlots];      // stack of boundary events
   uint8_t lc[kSlots];      // stack of real collisions
@@ -86,50 +92,51 @@ __device__ __forceinline__ V3 normal_of(uint32_t c) {
 template <int kSlots>
 __device__ __forceinline__ void store_full(WavePool<kSlots>& S, uint32_t s, const PathState& ps, const Isect& is,
                                            uint32_t nseg) {
-  S.ox[s] = ps.o.x;
-  S.oy[s] = ps.o.y;
-  S.oz[s] = ps.o.z;
-  S.dx[s] = ps.d.x;
-  S.dy[s] = ps.d.y;
-  S.dz[s] = ps.d.z;
-  S.tx[s] = ps.T.x;
-  S.ty[s] = ps.T.y;
-  S.tz[s] = ps.T.z;
-  S.dist[s] = is.dist;
-  S.t[s] = 0.0f;
-  S.r0[s] = ps.rng.v0;
-  S.r1[s] = ps.rng.v1;
-  S.r2[s] = ps.rng.v2;
-  S.r3[s] = ps.rng.v3;
-  S.r4[s] = ps.rng.v4;
-  S.rd[s] = ps.rng.d;
-  S.img[s] = ps.image_id;
-  S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
+  PoolSlot& q = S.p[s];
+  q.a = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
+  q.b = make_float4(ps.d.x, ps.d.y, ps.d.z, is.dist);
+  q.c = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);
+  q.e = make_uint4(ps.rng.v4, ps.rng.d, ps.image_id, normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4));
+  q.f = make_float4(ps.T.x, ps.T.y, ps.T.z, 0.0f);
 }
 template <int kSlots>
 __device__ __forceinline__ void load_full(const WavePool<kSlots>& S, uint32_t s, PathState& ps, Isect& is, uint32_t& nseg,
                                           float& t) {
-  ps.o = mk3(S.ox[s], S.oy[s], S.oz[s]);
-  ps.d = mk3(S.dx[s], S.dy[s], S.dz[s]);
-  ps.T = mk3(S.tx[s], S.ty[s], S.tz[s]);
-  is.dist = S.dist[s];
-  t = S.t[s];
-  ps.rng = Rng{S.r0[s], S.r1[s], S.r2[s], S.r3[s], S.r4[s], S.rd[s]};
-  ps.image_id = S.img[s];
-  const uint32_t meta = S.meta[s];
-  is.normal = normal_of(meta & 7u);
-  is.inside = (meta & 8u) != 0u;
-  nseg = meta >> 4;
+  const PoolSlot& q = S.p[s];
+  const float4 a = q.a, b = q.b, f = q.f;
+  const uint4 c = q.c, e = q.e;
+  ps.o = mk3(a.x, a.y, a.z);
+  t = a.w;
+  ps.d = mk3(b.x, b.y, b.z);
+  is.dist = b.w;
+  ps.T = mk3(f.x, f.y, f.z);
+  ps.rng = Rng{c.x, c.y, c.z, c.w, e.x, e.y};
+  ps.image_id = e.z;
+  is.normal = normal_of(e.w & 7u);
+  is.inside = (e.w & 8u) != 0u;
+  nseg = e.w >> 4;
 }
 template <int kSlots>
 __device__ __forceinline__ void store_track(WavePool<kSlots>& S, uint32_t s, float t, const Rng& rng) {
-  S.t[s] = t;
-  S.r0[s] = rng.v0;
-  S.r1[s] = rng.v1;
-  S.r2[s] = rng.v2;
-  S.r3[s] = rng.v3;
-  S.r4[s] = rng.v4;
-  S.rd[s] = rng.d;
+  PoolSlot& q = S.p[s];
+  q.a.w = t;
+  q.c = make_uint4(rng.v0, rng.v1, rng.v2, rng.v3);
+  q.e.x = rng.v4;
+  q.e.y = rng.d;
+}
+// Track state of a ready path: o, t, d, max_t, rng.
+template <int kSlots>
+__device__ __forceinline__ void load_track(const WavePool<kSlots>& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
+                                           float& max_t) {
+  const PoolSlot& q = S.p[s];
+  const float4 a = q.a, b = q.b;
+  const uint4 c = q.c;
+  const uint2 e = make_uint2(q.e.x, q.e.y);
+  o = mk3(a.x, a.y, a.z);
+  t = a.w;
+  d = mk3(b.x, b.y, b.z);
+  max_t = b.w;
+  rng = Rng{c.x, c.y, c.z, c.w, e.x, e.y};
 }
 
 enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
@@ -222,11 +229,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           const uint32_t r = ready_head + rank;
           const uint32_t s = S.ready[r >= (uint32_t)kSlots ? r - kSlots : r];
           slot = (int)s;
-          o = mk3(S.ox[s], S.oy[s], S.oz[s]);
-          d = mk3(S.dx[s], S.dy[s], S.dz[s]);
-          rng = Rng{S.r0[s], S.r1[s], S.r2[s], S.r3[s], S.r4[s], S.rd[s]};
-          t = S.t[s];
-          max_t = S.dist[s];
+          load_track(S, s, o, d, rng, t, max_t);
         }
         ready_head += k;
         if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
