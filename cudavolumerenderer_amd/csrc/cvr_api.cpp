@@ -73,6 +73,7 @@ struct cvr_ctx {
   bool use_cells = true;
   uint8_t* d_bounds = nullptr;  // brick bounds (MediumParams::bounds)
   uint32_t bound_shift = 2;     // log2 brick size, 0 = off
+  bool bound_shift_set = false; // CVR_OPT_BOUNDS given (else sparse media use 8^3 bricks)
   size_t n_voxels = 0;
   // sparse medium (cvr_set_medium_sparse)
   uint32_t* d_leaves = nullptr;
@@ -645,7 +646,10 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
   // bricks of 2^bshift <= 8 cells (within one leaf); bounds off -> q = 255
   const float sigma = sd->scale * sd->max_density;
   const int unbounded = !(c->bound_shift && sigma > 0.0f && std::isfinite(sigma) && sd->scale > 0.0f);
-  m.bshift = c->bound_shift == 0 ? 2u : std::min(c->bound_shift, 3u);
+  // Default 8^3 cells per brick: one brick word per leaf's cells (C5: 16.8 MB
+  // of words instead of 268 MB at 4^3, so they stay in L2 / Infinity Cache;
+  // 12% faster at an unchanged fetch rate, clouds being empty or dense).
+  m.bshift = !c->bound_shift_set ? 3u : c->bound_shift == 0 ? 2u : std::min(c->bound_shift, 3u);
   const uint32_t B = 1u << m.bshift;
   m.bnx = (res[0] + B - 1) / B;
   m.bny = (res[1] + B - 1) / B;
@@ -814,6 +818,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       // takes effect at the next cvr_set_medium
       if (v < 0 || v > 5) return set_err(&c->err, CVR_ERR_INVALID, "bounds must be 0 (off) or log2 brick size 1..5");
       c->bound_shift = (uint32_t)v;
+      c->bound_shift_set = true;
       return CVR_OK;
     case CVR_OPT_CELLS:
       // takes effect at the next cvr_set_medium

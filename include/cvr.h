@@ -74,8 +74,9 @@ typedef enum {
   CVR_OPT_WAVES = 10,         /* persistent kernel register budget: 4 (default), 5, 6, 8 waves/SIMD */
   CVR_OPT_ORDER = 11,         /* 1 (default): 8x8-pixel blocks, samples innermost; 0: path-id order */
   CVR_OPT_QUEUES = 12,        /* work bands / queues, one per XCD (default 8) */
-  CVR_OPT_BOUNDS = 13,        /* brick bounds: log2 brick size 1..5, 0 = off (default 2);
-                                 next cvr_set_medium.  Results are identical either way. */
+  CVR_OPT_BOUNDS = 13,        /* brick bounds: log2 brick size 1..5, 0 = off (default 2 dense,
+                                 3 sparse; sparse caps at 3); next cvr_set_medium.  Results are
+                                 identical either way. */
   CVR_OPT_TAIL = 14,          /* pool scheduler: lanes below which a wave ends a track phase (16) */
   CVR_OPT_BATCH = 15          /* wave-pool scheduler: idle lanes that trigger a refill (8) */
 } cvr_option;

@@ -65,7 +65,10 @@ def main():
         c.set_option(cvr.OPT_CELLS, d.get("cells", 1))
         if "bounds" in d:
             c.set_option(cvr.OPT_BOUNDS, d["bounds"])
-        c.set_medium(scene.medium)
+        if scene.is_sparse:
+            c.set_medium_sparse(scene.sparse_medium)
+        else:
+            c.set_medium(scene.medium)
         c.set_camera(iv, r2v, (W, H))
         if "ev" in d:
             c.set_option(cvr.OPT_EVENT_THRESHOLD, d["ev"])
