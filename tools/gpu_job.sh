@@ -43,6 +43,8 @@ for step in "$@"; do
     pmc_c) run pmc_c 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc_c" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     pmc_f) run pmc_f 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_f" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     pmc_w) run pmc_w 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_w" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
+    pmc_d) run pmc_d 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_IFETCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_LDS_BANK_CONFLICT --kernel-trace -d "$OUT/pmc_d" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
+    pmc_e) run pmc_e 90 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES --kernel-trace -d "$OUT/pmc_e" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     # per-scene profiles: prof:SCENE, pmcf:SCENE (FETCH_SIZE), pmcw:SCENE (WRITE_SIZE)
     prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmcf:*) sc=${step#pmcf:}; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;

@@ -65,7 +65,7 @@ def main():
         c.set_option(cvr.OPT_CELLS, d.get("cells", 1))
         if "bounds" in d:
             c.set_option(cvr.OPT_BOUNDS, d["bounds"])
-        if scene.is_sparse:
+        if scene.is_sparse or d.get("sparse", 0):
             c.set_medium_sparse(scene.sparse_medium)
         else:
             c.set_medium(scene.medium)
