@@ -144,6 +144,31 @@ def test_render_tiles_sharded_sums_to_render_image(cvr, scenes, kernel, world):
     assert_pixels_close(total, np.nan_to_num(img0), iters)
 
 
+@pytest.mark.parametrize("kernel", ["regenerationSK", "streamingSK", "naiveSK"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_tile_path_shards_sum_to_render_image(cvr, scenes, kernel, world):
+    """bench.py --shard tilepaths: rank r renders path-id shard r of every
+    tile (cvr_set_path_range + cvr_render_tiles, each tile with its own seed);
+    the ranks' images sum to the sequential tile loop's (rgb; w is a plain
+    store per render)."""
+    from cudavolumerenderer_amd.distributed import shard_range
+    scene = scenes["manix_small"]
+    W, H, iters, tiles = 128, 96, 3, (4, 2)
+    ref, _, _ = make_ctx(cvr, scene, W, H, kernel, seed=5)
+    img0, st0 = ref.render_image(W, H, tiles, iters)
+    total = np.zeros_like(img0[..., :3])
+    steps = paths = 0
+    for r in range(world):
+        ctx, _, _ = make_ctx(cvr, scene, W, H, kernel, seed=5)
+        ctx.set_path_range(*shard_range((W // 4) * (H // 2) * iters, r, world))
+        img, st = ctx.render_tiles(W, H, tiles, iters, 0, 1)
+        total += np.nan_to_num(img[..., :3])
+        steps += st.steps
+        paths += st.paths
+    assert steps == st0.steps and paths == st0.paths
+    assert_pixels_close(total, np.nan_to_num(img0[..., :3]), world * iters)
+
+
 def test_c1_bucky_256_4it(cvr, oracle_mod, scenes):
     """BASELINE config C1 (bucky 32^3, 256x256, 4 iterations) through naiveSK."""
     scene = scenes["bucky"]
