@@ -1003,7 +1003,11 @@ int cvr_render_tiles(cvr_ctx* c, const cvr_render_desc* d, uint32_t first_tile, 
   float4* tmp_img = nullptr;
   if (!dimg && host_image) {
     HIP_TRY(c, hipMalloc(&tmp_img, (size_t)W * H * sizeof(float4)));
-    HIP_TRY(c, hipMemsetAsync(tmp_img, 0, (size_t)W * H * sizeof(float4), c->stream));
+    const hipError_t e = hipMemsetAsync(tmp_img, 0, (size_t)W * H * sizeof(float4), c->stream);
+    if (e != hipSuccess) {
+      (void)hipFree(tmp_img);
+      return set_err(&c->err, CVR_ERR_HIP, "image buffer: %s", hipGetErrorString(e));
+    }
     dimg = tmp_img;
   }
   const uint32_t seed0 = c->seed;
