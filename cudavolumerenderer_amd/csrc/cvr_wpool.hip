@@ -35,6 +35,15 @@
 #ifndef CVR_WPOOL_UNROLL
 #define CVR_WPOOL_UNROLL 4
 #endif
+// Wave priorities (s_setprio): the track loop above the event code, so a
+// stepping wave issues its brick-bound and cell loads ahead of the
+// VALU-dense event batches of the other waves on its SIMD (C2: -0.7%).
+#ifndef CVR_PRIO_TRACK
+#define CVR_PRIO_TRACK 1
+#endif
+#ifndef CVR_PRIO_EVENT
+#define CVR_PRIO_EVENT 0
+#endif
 
 namespace cvr {
 
@@ -196,6 +205,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
   for (;;) {
     // ================================================= TRACK ==============
+    __builtin_amdgcn_s_setprio(CVR_PRIO_TRACK);
     // The track state is fresh per outer iteration and parked in the pool
     // before the event code runs, so nothing of it is live across that code
     // (keeps the step loop free of spills).
@@ -295,6 +305,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     if (n_lb + n_lc == 0u && n_ready == 0u && (n_ln == 0u || cur.exhausted)) break;
 
     // ================================================= EVENT ==============
+    __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
     // One batch of up to 64 items, [boundary | collision | new].  New items
     // are regenerated first: a camera path's first segment is an AABB test
     // and, when it hits the box from outside, a boundary event, which then
