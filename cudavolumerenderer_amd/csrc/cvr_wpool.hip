@@ -190,7 +190,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
   // event cycles, track cycles, event batches, track iterations, event-code cycles, regen+AABB cycles,
   // load, boundary, collision, regeneration cycles
-  unsigned long long st[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // + batch composition: boundary-only, collision-only, mixed batches; boundary, collision, new lanes
+  unsigned long long st[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define CVR_LAP(k)                                              \
   {                                                             \
     const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
@@ -316,23 +317,40 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     // slot in the new list for a later batch.
     {
 // Kind-major batches: once 40 boundary (else collision) events wait, the
-// batch runs that kind alone (plus new paths), so its code runs on more
-// lanes; otherwise [boundary | collision | new] as they come (C2: -1.5%).
+// batch runs that kind alone, so its code runs on more lanes; otherwise
+// [boundary | collision | new] as they come (C2: -1.5%).  New paths fill a
+// boundary batch (a camera path's first event is its GGX entry into the box,
+// the same code) but not a collision batch unless CVR_WPOOL_NEW_FORCE wait:
+// beside collisions they would run the whole boundary code on a few lanes
+// (C2 -2.7%, C3 -3%).
 #ifndef CVR_WPOOL_KIND_MIN
 #define CVR_WPOOL_KIND_MIN 40
 #endif
-      uint32_t tb, tc;
+#ifndef CVR_WPOOL_NEW_FORCE
+#define CVR_WPOOL_NEW_FORCE 64
+#endif
+      uint32_t tb, tc, tn;
       if (CVR_WPOOL_KIND_MIN > 0 && n_lb >= (uint32_t)CVR_WPOOL_KIND_MIN) {
         tb = min(n_lb, 64u);
         tc = 0;
+        tn = min(n_ln, 64u - tb);
       } else if (CVR_WPOOL_KIND_MIN > 0 && n_lc >= (uint32_t)CVR_WPOOL_KIND_MIN) {
         tb = 0;
         tc = min(n_lc, 64u);
+        tn = n_ln < (uint32_t)CVR_WPOOL_NEW_FORCE ? 0u : min(n_ln, 64u - tc);
       } else {
         tb = min(n_lb, 64u);
         tc = min(n_lc, 64u - tb);
+        tn = min(n_ln, 64u - tb - tc);
       }
-      const uint32_t tn = min(n_ln, 64u - tb - tc);
+#if CVR_STAMPS
+      st[10] += (tb > 0u && tc == 0u);
+      st[11] += (tc > 0u && tb == 0u);
+      st[12] += (tb > 0u && tc > 0u);
+      st[13] += tb;
+      st[14] += tc;
+      st[15] += tn;
+#endif
       uint32_t kind = K_NONE, s = 0;
       if (lane < tb) {
         kind = K_BOUNDARY;
@@ -506,7 +524,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     st[1] += now - t_mark;
   }
   if (lane == 0)
-    for (int k = 0; k < 10; ++k) atomicAdd(L.stats + 16 + k, st[k]);
+    for (int k = 0; k < 16; ++k) atomicAdd(L.stats + 16 + k, st[k]);
 #endif
 }
 

@@ -11,7 +11,7 @@ shift 2
 for v in "$@"; do
   if [ "$v" = default ]; then L=""; else L="--lib build/variants/$v/libcvr.so"; fi
   echo "== $v ($scene)"
-  timeout -k 10 150 python3 tools/tune.py $L --scene "$scene" --rounds "$rounds" --variants "regenerationSK:" \
+  timeout -k 10 150 python3 tools/tune.py $L --scene "$scene" ${AB_ARGS:-} --rounds "$rounds" --variants "regenerationSK:" \
     > /tmp/ab_$$.log 2>&1 || { cat /tmp/ab_$$.log; exit 1; }
   grep regen /tmp/ab_$$.log
 done

@@ -30,6 +30,7 @@ for batch in [8]:
     out = (C.c_uint64 * 16)()
     lib.cvr_debug_counters(c._h, out)
     ev, tr, n_ev, n_tr, ev_code, ev_to_regen_end, c_load, c_bnd, c_col, c_regen = list(out)[:10]
+    b_only, c_only, mixed, lanes_b, lanes_c, lanes_n = list(out)[10:16]
     tot = ev + tr
     print(f"batch {batch}: kernel {st.kernel_ms:.2f} ms; event share {ev / tot:.3f}; event batches {n_ev} "
           f"({ev / max(n_ev, 1):.0f} cyc each, {(st.segments + st.paths) / max(n_ev, 1):.1f} items each); "
@@ -39,3 +40,7 @@ for batch in [8]:
           f"load {c_load / max(n_ev, 1):.0f} boundary {c_bnd / max(n_ev, 1):.0f} collision {c_col / max(n_ev, 1):.0f} "
           f"regen {c_regen / max(n_ev, 1):.0f} AABB+store {(ev_to_regen_end - c_load - c_bnd - c_col - c_regen) / max(n_ev, 1):.0f}",
           flush=True)
+    nb = max(n_ev, 1)
+    print(f"batches: boundary-only {b_only / nb:.3f}, collision-only {c_only / nb:.3f}, mixed {mixed / nb:.3f}, "
+          f"neither {(n_ev - b_only - c_only - mixed) / nb:.3f}; lanes per batch: boundary {lanes_b / nb:.1f} "
+          f"collision {lanes_c / nb:.1f} new {lanes_n / nb:.1f}", flush=True)
