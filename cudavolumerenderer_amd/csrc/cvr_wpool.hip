@@ -316,15 +316,19 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     // item loops: a path that dies (roulette, escape, truncation) files its
     // slot in the new list for a later batch.
     {
-// Kind-major batches: once 40 boundary (else collision) events wait, the
+// Kind-major batches: once 48 boundary (else 24 collision) events wait, the
 // batch runs that kind alone, so its code runs on more lanes; otherwise
-// [boundary | collision | new] as they come (C2: -1.5%).  New paths fill a
+// [boundary | collision | new] as they come (C2: -1.5% at 40/40, then -1.3%
+// at 48/24).  New paths fill a
 // boundary batch (a camera path's first event is its GGX entry into the box,
 // the same code) but not a collision batch unless CVR_WPOOL_NEW_FORCE wait:
 // beside collisions they would run the whole boundary code on a few lanes
 // (C2 -2.7%, C3 -3%).
 #ifndef CVR_WPOOL_KIND_MIN
-#define CVR_WPOOL_KIND_MIN 40
+#define CVR_WPOOL_KIND_MIN 48
+#endif
+#ifndef CVR_WPOOL_KIND_MIN_C
+#define CVR_WPOOL_KIND_MIN_C 24
 #endif
 #ifndef CVR_WPOOL_NEW_FORCE
 #define CVR_WPOOL_NEW_FORCE 64
@@ -334,7 +338,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         tb = min(n_lb, 64u);
         tc = 0;
         tn = min(n_ln, 64u - tb);
-      } else if (CVR_WPOOL_KIND_MIN > 0 && n_lc >= (uint32_t)CVR_WPOOL_KIND_MIN) {
+      } else if (CVR_WPOOL_KIND_MIN_C > 0 && n_lc >= (uint32_t)CVR_WPOOL_KIND_MIN_C) {
         tb = 0;
         tc = min(n_lc, 64u);
         tn = n_ln < (uint32_t)CVR_WPOOL_NEW_FORCE ? 0u : min(n_ln, 64u - tc);
