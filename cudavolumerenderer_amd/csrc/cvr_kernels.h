@@ -50,9 +50,6 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
                         hipStream_t s);
 hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
-// The tile's pixels outside the active block rectangle of an order-1 launch
-// (LaunchParams::ab_x0): one (1, 1, 1) splat per sample, counters included.
-hipError_t launch_background(const LaunchParams& L, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);
 // Sparse medium: cell-leaf pool (`coords`: 3 u32 leaf coordinates per slot,

@@ -8,8 +8,6 @@
 // The production regenerationSK scheduler is cvr_persistent.hip.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-
 #include "cvr_kernels.h"
 #include "cvr_walk.h"
 
@@ -177,44 +175,6 @@ __global__ __launch_bounds__(256) void k_tile_to_image(const float4* __restrict_
   image[(size_t)(y + oy) * iw + (x + ox)] = make_float4(v.x / scale, v.y / scale, v.z / scale, v.w / scale);
 }
 
-// ----------------------------------------------------------- background ---
-// Pixels of the tile outside the active block rectangle (LaunchParams
-// ab_x0/ab_y0/blocks_x/n_blocks): every camera ray of these pixels misses the
-// box (cvr_api.cpp active_blocks proves it with a margin), so each of their
-// paths ends at its first AABB test and splats T = (1, 1, 1)
-// (NaiveVolPTsk_kernel.cuh:33-47, atomicVectorAdd).  The same sums, in the
-// same order (one 1.0f per sample), without the walk; the counters get one
-// path, one segment and one escape per path.
-__global__ __launch_bounds__(256) void k_background(LaunchParams L) {
-  const uint32_t abh = L.n_blocks / L.blocks_x;
-  const uint32_t tile_h = L.tile_px / L.tile_w;
-  uint32_t n = 0;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < L.tile_px; i += gridDim.x * 256) {
-    const uint32_t x = i % L.tile_w, y = i / L.tile_w;
-    const uint32_t bx = x >> 3, by = y >> 3;
-    const bool active = y < tile_h && bx >= L.ab_x0 && bx < L.ab_x0 + L.blocks_x && by >= L.ab_y0 &&
-                        by < L.ab_y0 + abh;
-    if (active) continue;
-    float4 v = L.out[i];
-    for (uint32_t s = 0; s < L.samples; ++s) {
-      v.x += 1.0f;
-      v.y += 1.0f;
-      v.z += 1.0f;
-    }
-    v.w = 1.0f;
-    L.out[i] = v;
-    n += L.samples;
-  }
-  unsigned long long t = n;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
-  if ((threadIdx.x & 63u) == 0 && t) {
-    atomicAdd(L.stats + STAT_PATHS, t);
-    atomicAdd(L.stats + STAT_SEGMENTS, t);
-    atomicAdd(L.stats + STAT_ESCAPED, t);
-  }
-}
-
 // ----------------------------------------------------------- cell table ---
 // Corner-replicated density cells (see MediumParams::cells).
 __global__ __launch_bounds__(256) void k_build_cells(const float* __restrict__ D, uint32_t rx, uint32_t ry,
@@ -348,13 +308,6 @@ hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatt
     hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(256), 0, s, m, L, rec);
   else
     hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(256), 0, s, m, L, rec);
-  return hipGetLastError();
-}
-
-hipError_t launch_background(const LaunchParams& L, hipStream_t s) {
-  if (L.tile_px == 0 || L.samples == 0) return hipSuccess;
-  const uint32_t grid = std::min<uint32_t>((L.tile_px + 255u) / 256u, 1024u);
-  hipLaunchKernelGGL(k_background, dim3(grid), dim3(256), 0, s, L);
   return hipGetLastError();
 }
 

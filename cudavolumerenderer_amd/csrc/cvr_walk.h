@@ -179,11 +179,6 @@ struct LaunchParams {
   uint32_t blocks_x;      // tile_w / 8
   uint32_t n_blocks;      // tile_px / 64
   uint32_t n_queues;      // 1..8
-  // Order 1 covers the blocks of a rectangle of the tile: blocks_x x
-  // (n_blocks / blocks_x) blocks from block (ab_x0, ab_y0).  The whole tile
-  // unless the launch proved the other blocks' camera rays all miss the box
-  // (cvr_api.cpp active_blocks; k_background renders those).
-  uint32_t ab_x0, ab_y0;
   uint32_t qbeg[9];       // first block of each queue's band (order 1), qbeg[n_queues] = n_blocks
   FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x;  // by tile_px, tile_w, 64*samples, blocks_x
 };
@@ -204,7 +199,7 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   const uint32_t rem = u - bq * per_block;
   const uint32_t s = rem >> 6, lane = rem & 63u;
   const uint32_t by = fastdiv(b, L.div_blocks_x);
-  const uint32_t px = (L.ab_x0 + b - by * L.blocks_x) * 8u + (lane & 7u), py = (L.ab_y0 + by) * 8u + (lane >> 3);
+  const uint32_t px = (b - by * L.blocks_x) * 8u + (lane & 7u), py = by * 8u + (lane >> 3);
   return L.path_first + s * L.tile_px + py * L.tile_w + px;
 }
 

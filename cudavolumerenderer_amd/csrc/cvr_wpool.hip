@@ -318,8 +318,9 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     {
 // Kind-major batches: once 48 boundary (else 24 collision) events wait, the
 // batch runs that kind alone, so its code runs on more lanes; otherwise
-// [boundary | collision | new] as they come (C2: -1.5% at 40/40, then -1.3%
-// at 48/24).  New paths fill a
+// [boundary | collision | new] as they come (C2: -1.5% at 40/40; 48/24 is
+// a further -1.8% on C2 and -1.0% on C3, profiles/round2/ab_kindmin_*.log).
+// New paths fill a
 // boundary batch (a camera path's first event is its GGX entry into the box,
 // the same code) but not a collision batch unless CVR_WPOOL_NEW_FORCE wait:
 // beside collisions they would run the whole boundary code on a few lanes

@@ -49,6 +49,8 @@ for step in "$@"; do
     prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmcf:*) sc=${step#pmcf:}; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcw:*) sc=${step#pmcw:}; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    # A/B of experiment builds: ab:SCENE:ROUNDS:variant1,variant2,...
+    ab:*) IFS=: read -r _ sc rounds vs <<< "$step"; run ab_$sc 400 bash tools/ab.sh $sc $rounds ${vs//,/ } ;;
     *) echo "unknown step $step" ;;
   esac
 done
