@@ -16,7 +16,7 @@ SRCS_CPP := $(CSRC)/cvr_api.cpp $(CSRC)/cvr_scene.cpp $(CSRC)/cvr_vdb.cpp $(CSRC
 OBJS := $(patsubst $(CSRC)/%.hip,$(OBJDIR)/%.o,$(SRCS_HIP)) $(patsubst $(CSRC)/%.cpp,$(OBJDIR)/%.o,$(SRCS_CPP))
 HDRS := include/cvr.h include/cvr_detmath.h $(wildcard $(CSRC)/*.h)
 
-all: $(PKG)/libcvr.so $(PKG)/cvr oracle
+all: $(PKG)/libcvr.so $(PKG)/cvr build/launcher_order oracle
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -31,6 +31,13 @@ $(PKG)/libcvr.so: $(OBJS)
 
 $(PKG)/cvr: $(CSRC)/cvr_main.cpp $(PKG)/libcvr.so include/cvr.h
 	g++ -O2 -std=c++17 -Iinclude -o $@ $< -L$(PKG) -lcvr -Wl,-rpath,'$$ORIGIN'
+
+# Host-only C++ test: libcvr driven through include/cvr_launcher.hpp in
+# CudaVolPath's call order (tests/test_launcher_adapter.py).
+build/launcher_order: tests/cpp/launcher_order.cpp include/cvr_launcher.hpp include/cvr.h $(PKG)/libcvr.so
+	@mkdir -p build
+	g++ -O2 -std=c++17 -Wall -D__HIP_PLATFORM_AMD__ -Iinclude -I/opt/rocm/include -o $@ $< \
+	    -L$(PKG) -lcvr -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,'$$ORIGIN/../$(PKG)' -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

@@ -695,6 +695,9 @@ int cvr_set_resolution(cvr_ctx* c, uint32_t w, uint32_t h) {
   if (w == 0 || h == 0) return set_err(&c->err, CVR_ERR_INVALID, "zero tile resolution");
   if ((uint64_t)w * h > (1ull << 24))
     return set_err(&c->err, CVR_ERR_INVALID, "tile of %ux%u exceeds 2^24 pixels (float pixel indexing)", w, h);
+  if ((uint64_t)w * h * c->iterations > 0xFFFFFFFFull)
+    return set_err(&c->err, CVR_ERR_INVALID, "n_paths = %llu exceeds the reference's uint32 path ids",
+                   (unsigned long long)((uint64_t)w * h * c->iterations));
   c->tile_w = w;
   c->tile_h = h;
   c->n_paths = (uint64_t)w * h * c->iterations;
@@ -859,6 +862,18 @@ int cvr_launch_render(cvr_ctx* c) {
   cvr::LaunchParams L{};
   fill_launch(c, L, first, count);
   const bool eps = scatter_eps_for(c);
+  // The persistent schedulers' u32 queue heads run past a queue's end by at
+  // most one chunk per wave before every wave sees the queue exhausted
+  // (waves: at most 4 per block of any scheduler).
+  const uint64_t waves_max =
+      4ull * (c->grid_override ? c->grid_override
+                               : (uint64_t)std::max({c->persistent_grid, c->pool_grid, c->wpool_grid}));
+  uint64_t units_max = L.order ? 0 : count;
+  for (uint32_t q = 0; L.order && q < L.n_queues; ++q)
+    units_max = std::max<uint64_t>(units_max, (uint64_t)(L.qbeg[q + 1] - L.qbeg[q]) * 64u * L.samples);
+  if (first + count > 0xFFFFFFFFull || units_max + waves_max * L.chunk > 0xFFFFFFFFull)
+    return set_err(&c->err, CVR_ERR_INVALID, "path range [%llu, +%llu) overflows the 32-bit path ids / queue heads",
+                   (unsigned long long)first, (unsigned long long)count);
   HIP_TRY(c, hipMemsetAsync(c->d_work, 0, kWorkBytes, c->stream));
   HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
   c->last_iterations = 0;

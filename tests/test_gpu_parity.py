@@ -335,6 +335,15 @@ def test_errors_are_reported_not_fatal(cvr, scenes):
     assert "CVR_ERR_STATE" in str(e.value)
     with pytest.raises(cvr.CvrError):
         ctx.set_option(cvr.OPT_EVENT_THRESHOLD, 0)
+    # n_paths must fit the reference's uint32 path ids whichever of
+    # setNIterations / setResolution comes last
+    ctx.set_resolution(16, 16)
+    ctx.set_iterations(256)
+    with pytest.raises(cvr.CvrError) as e:
+        ctx.set_resolution(4096, 4096)
+    assert "uint32" in str(e.value)
+    with pytest.raises(cvr.CvrError):
+        ctx.set_iterations(1 << 30)
 
 
 @pytest.mark.parametrize("scene_key", ["manix_small", "hetvol"])
