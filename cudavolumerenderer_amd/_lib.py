@@ -108,6 +108,7 @@ def load() -> C.CDLL:
         "cvr_set_offset": (I32, [P, U32, U32]),
         "cvr_set_iterations": (I32, [P, U32]),
         "cvr_set_path_range": (I32, [P, U64, U64]),
+        "cvr_set_block_shard": (I32, [P, U32, U32]),
         "cvr_set_seed": (I32, [P, U32]),
         "cvr_get_seed": (I32, [P, C.POINTER(U32)]),
         "cvr_set_output": (I32, [P, P]),
@@ -346,6 +347,10 @@ class Context:
 
     def set_path_range(self, first, count):
         self._c(load().cvr_set_path_range(self._h, first, count))
+
+    def set_block_shard(self, rank, world):
+        """Launch only shard `rank` of `world` (cvr_set_block_shard)."""
+        self._c(load().cvr_set_block_shard(self._h, rank, world))
 
     def set_seed(self, seed):
         self._c(load().cvr_set_seed(self._h, seed))

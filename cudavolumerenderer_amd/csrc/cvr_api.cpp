@@ -94,6 +94,7 @@ struct cvr_ctx {
   uint32_t iterations = 1;
   uint64_t n_paths = 0;
   uint64_t range_first = 0, range_count = UINT64_MAX;
+  uint32_t shard_rank = 0, shard_world = 1;  // cvr_set_block_shard
   uint32_t seed = 0;
 
   float4* d_out_owned = nullptr;
@@ -210,7 +211,19 @@ static cvr::FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
-void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_t count) {
+void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_t count, bool sharded = true) {
+  const uint32_t shard_world = sharded ? c->shard_world : 1u;
+  const uint64_t P0 = (uint64_t)(uint32_t)((float)c->tile_w * (float)c->tile_h);
+  // the persistent schedulers take work units through unit_to_path (pixel-block order); naiveSK/MK
+  // and the wavefront pair map launch index -> path id directly
+  const bool queued = c->kernel != CVR_KERNEL_NAIVE_SK && c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1;
+  const bool block_order = queued && c->order && P0 && first % P0 == 0 && count % P0 == 0 && count > 0 &&
+                           c->tile_w % 8 == 0 && c->tile_h % 8 == 0;
+  if (shard_world > 1 && !block_order) {  // no block order: a contiguous share of the path ids
+    const uint64_t base = count / c->shard_world, rem = count % c->shard_world;
+    first += c->shard_rank * base + std::min<uint64_t>(c->shard_rank, rem);
+    count = base + (c->shard_rank < rem ? 1 : 0);
+  }
   memcpy(L.M, c->inv_view, sizeof(L.M));
   L.r2v[0] = c->r2v[0];
   L.r2v[1] = c->r2v[1];
@@ -238,12 +251,21 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   // contiguous band of blocks per queue, when the launch covers whole samples
   const uint64_t P = L.tile_px;
   const bool aligned = P && first % P == 0 && count % P == 0 && count > 0;
+  L.blk_off = 0;
+  L.blk_stride = 1;
   if (c->order && aligned && c->tile_w % 8 == 0 && c->tile_h % 8 == 0) {
     L.order = 1;
     L.samples = (uint32_t)(count / P);
     L.blocks_x = c->tile_w / 8;
     L.n_blocks = (uint32_t)(P / 64);
+    if (shard_world > 1 && block_order) {  // blocks shard_rank, shard_rank + world, ...
+      L.blk_off = c->shard_rank;
+      L.blk_stride = c->shard_world;
+      L.n_blocks = L.n_blocks > c->shard_rank ? (L.n_blocks - c->shard_rank + c->shard_world - 1) / c->shard_world : 0;
+      L.path_count = L.n_blocks * 64u * L.samples;
+    }
     L.n_queues = c->n_queues < L.n_blocks ? c->n_queues : L.n_blocks;
+    if (L.n_queues == 0) L.n_queues = 1;
   } else {
     L.order = 0;
     L.samples = 0;
@@ -729,6 +751,14 @@ int cvr_set_path_range(cvr_ctx* c, uint64_t first, uint64_t count) {
   return CVR_OK;
 }
 
+int cvr_set_block_shard(cvr_ctx* c, uint32_t rank, uint32_t world) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  if (world == 0 || rank >= world) return set_err(&c->err, CVR_ERR_INVALID, "bad shard %u of %u", rank, world);
+  c->shard_rank = rank;
+  c->shard_world = world;
+  return CVR_OK;
+}
+
 int cvr_set_seed(cvr_ctx* c, uint32_t seed) {
   if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
   c->seed = seed;
@@ -985,7 +1015,7 @@ int cvr_trace_paths(cvr_ctx* c, uint32_t first, uint32_t count, cvr_path_record*
   if (r) return r;
   if (count == 0) return CVR_OK;
   cvr::LaunchParams L{};
-  fill_launch(c, L, first, count);
+  fill_launch(c, L, first, count, /*sharded=*/false);
   cvr::PathRecord* d_rec = nullptr;
   HIP_TRY(c, hipMalloc(&d_rec, (size_t)count * sizeof(cvr::PathRecord)));
   hipError_t e = cvr::launch_trace(c->m, L, scatter_eps_for(c), d_rec, c->stream);

@@ -177,8 +177,12 @@ struct LaunchParams {
   uint32_t order;
   uint32_t samples;       // path_count / tile_px (order 1)
   uint32_t blocks_x;      // tile_w / 8
-  uint32_t n_blocks;      // tile_px / 64
+  uint32_t n_blocks;      // blocks of this launch: tile_px / 64 (or the block shard's share)
   uint32_t n_queues;      // 1..8
+  // Block shard (cvr_set_block_shard): this launch's blocks are the tile's
+  // blocks blk_off, blk_off + blk_stride, ...; local block b is tile block
+  // blk_off + b * blk_stride (0 / 1: the whole tile).
+  uint32_t blk_off, blk_stride;
   uint32_t qbeg[9];       // first block of each queue's band (order 1), qbeg[n_queues] = n_blocks
   FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x;  // by tile_px, tile_w, 64*samples, blocks_x
 };
@@ -195,7 +199,7 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.order == 0) return L.path_first + u;
   const uint32_t per_block = 64u * L.samples;
   const uint32_t bq = fastdiv(u, L.div_block);
-  const uint32_t b = queue_blocks_begin(L, q) + bq;
+  const uint32_t b = L.blk_off + __umul24(queue_blocks_begin(L, q) + bq, L.blk_stride);
   const uint32_t rem = u - bq * per_block;
   const uint32_t s = rem >> 6, lane = rem & 63u;
   const uint32_t by = fastdiv(b, L.div_blocks_x);

@@ -50,21 +50,15 @@ namespace cvr {
 namespace {
 
 // Paths per wave for a register/LDS budget of kWaves waves per SIMD: pool +
-// launch parameters must fit 160 KB / (4 kWaves) of LDS (125 slots at 4 waves
-// per SIMD, 96 at 5).
+// launch parameters must fit 160 KB / (4 kWaves) of LDS, or the CU holds
+// fewer waves than the register budget allows (round 1 lost 7% to an 8-byte
+// LaunchParams growth that pushed the workgroup to 10248 bytes).  Derived from
+// sizeof(LaunchParams): 118 slots at 4 waves per SIMD, 94 at 5, 158 at 3.
 template <int kWaves>
-struct PoolSize;
-template <>
-struct PoolSize<3> {
-  static constexpr int value = 159;
-};
-template <>
-struct PoolSize<4> {
-  static constexpr int value = 119;
-};
-template <>
-struct PoolSize<5> {
-  static constexpr int value = 94;
+struct PoolSize {
+  static constexpr int kBudget = 163840 / (4 * kWaves);  // LDS bytes per one-wave workgroup
+  static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
+  static constexpr int value = (kBudget - kParams - 16) / (80 + 4);  // 80-byte slot + 4 list bytes
 };
 
 // One path per slot, array-of-structs in 16-byte blocks so a path moves with
@@ -170,6 +164,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
   }
+  static_assert(sizeof(WavePool<kSlots>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
+                "wave pool exceeds the LDS budget of kWaves waves per SIMD");
   __shared__ WavePool<kSlots> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's

@@ -25,9 +25,18 @@ Tiles x paths (the third mode, `bench.py --shard tilepaths`): every rank
 renders its path-id shard of every tile, each tile with its sequential-loop
 seed, so the work splits evenly whatever the tile costs; the all-reduce sums
 the ranks' partial images (linear in the paths).
+
+Block shards (cvr_set_block_shard; bench.py's default strong-scaling mode):
+rank r renders the 8x8 pixel blocks r, r+world, ... of the tile with all
+their samples, so every rank keeps the pixel-block work order of the single-
+GPU kernel and sees the whole image (balanced whatever the scene); the ranks'
+path-id sets partition the launch (block_shard_path_ids), and one
+reduce-scatter sums the partial images.
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import Callable, Tuple
 
 
@@ -95,3 +104,112 @@ def render_tile_paths_sharded(render_tiles_range: Callable[[int, int], "object"]
     if world > 1 and all_reduce is not None:
         all_reduce(img)
     return img
+
+
+def block_shard_path_ids(tile_w: int, tile_h: int, samples: int, rank: int, world: int, first_sample: int = 0):
+    """Path ids rank `rank` renders under cvr_set_block_shard(rank, world) for
+    a launch of samples [first_sample, first_sample + samples) of a tile whose
+    sides are multiples of 8 (the pixel-block order): the pixels of blocks
+    rank, rank + world, ... (blocks row-major, 8x8 pixels each), every sample.
+    A restatement of fill_launch / unit_to_path for tests (numpy array)."""
+    import numpy as np
+    if tile_w % 8 or tile_h % 8:
+        raise ValueError("block shards need tile sides that are multiples of 8")
+    bx = tile_w // 8
+    nb = bx * (tile_h // 8)
+    blocks = np.arange(rank, nb, world)
+    lane = np.arange(64)
+    px = (blocks[:, None] % bx) * 8 + (lane[None, :] & 7)
+    py = (blocks[:, None] // bx) * 8 + (lane[None, :] >> 3)
+    pix = (py * tile_w + px).reshape(-1)
+    s = np.arange(first_sample, first_sample + samples)
+    return (s[:, None] * (tile_w * tile_h) + pix[None, :]).reshape(-1)
+
+
+def render_block_sharded(render_shard: Callable[[int, int], "object"], rank: int, world: int,
+                         reduce: Callable[["object"], "object"] | None):
+    """Render this rank's block shard (`render_shard(rank, world)` returns the
+    rank's unnormalised accumulator) and combine the ranks' accumulators with
+    `reduce` (a sum: all-reduce, reduce or reduce-scatter)."""
+    acc = render_shard(rank, world)
+    if world > 1 and reduce is not None:
+        return reduce(acc)
+    return acc
+
+
+class HostImage:
+    """The render's host image (the reference's buffer_out, Image.cpp:9-11
+    cudaHostAlloc): pinned memory.  With N ranks it is one /dev/shm mapping
+    shared by the node's processes, registered as pinned memory in each, and
+    rank r writes its slice [r*chunk, (r+1)*chunk) of the flat float array."""
+
+    def __init__(self, torch, dist, n_floats, rank, world, tag=None, pin=True):
+        import numpy as np
+        self.n = n_floats
+        self.chunk = -(-n_floats // world)
+        self.world = world
+        self.rank = rank
+        self.path = None
+        self._registered = False
+        if world == 1:
+            self.flat = torch.empty(n_floats, dtype=torch.float32, pin_memory=pin)
+            self.pinned = pin
+            return
+        run = tag or (os.environ.get("TORCHELASTIC_RUN_ID", "x") + "_" + os.environ.get("MASTER_PORT", "0"))
+        self.path = f"/dev/shm/cvr_bench_image_{run}"
+        nbytes = self.chunk * world * 4
+        if rank == 0:
+            mm = np.memmap(self.path, dtype=np.float32, mode="w+", shape=(self.chunk * world,))
+        dist.barrier()
+        if rank != 0:
+            mm = np.memmap(self.path, dtype=np.float32, mode="r+", shape=(self.chunk * world,))
+        self._mm = mm
+        self.flat = torch.from_numpy(mm)
+        self.pinned = False
+        try:  # hipHostRegister the mapping (plumbing; the copy is correct either way)
+            if not pin:
+                raise OSError("not pinned")
+            hip = ctypes.CDLL("libamdhip64.so")
+            hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+            self._hip = hip
+            if hip.hipHostRegister(ctypes.c_void_p(self.flat.data_ptr()), nbytes, 0) == 0:
+                self.pinned = self._registered = True
+        except OSError:
+            pass
+
+    def slice(self, r):
+        return self.flat[r * self.chunk:(r + 1) * self.chunk]
+
+    def close(self, dist):
+        if self._registered:
+            self._hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+            self._hip.hipHostUnregister(ctypes.c_void_p(self.flat.data_ptr()))
+        if self.path:
+            dist.barrier()
+            if self.rank == 0:
+                try:
+                    os.unlink(self.path)
+                except OSError:
+                    pass
+
+
+def reduce_to_host(acc_flat, part, host: HostImage, scale: float, dist):
+    """The end of one render over N ranks: sum the ranks' framebuffers
+    (`acc_flat`, padded to host.chunk * world floats) with one reduce-scatter,
+    normalise this rank's slice by `scale` (UtilityFunctors::Scale, x / scale,
+    Utilities.h:6-15) and copy it into its slice of the host image.  With one
+    rank: normalise and copy the whole framebuffer."""
+    if host.world > 1:
+        if acc_flat.is_cuda and dist.get_backend() == "gloo":
+            # gloo (the GPU tests' two ranks on one device): the collective on host copies
+            p = part.cpu()
+            dist.reduce_scatter_tensor(p, acc_flat.cpu())
+            part.copy_(p)
+        else:
+            dist.reduce_scatter_tensor(part, acc_flat)
+        mine = part
+    else:
+        mine = acc_flat
+    if scale != 1.0:
+        mine.div_(scale)
+    host.slice(host.rank).copy_(mine, non_blocking=host.pinned)

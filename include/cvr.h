@@ -172,6 +172,16 @@ int cvr_set_iterations(cvr_ctx* ctx, uint32_t iterations);
 /* Extension for sharding: launch only path ids [first, first+count) of the
  * tile's n_paths (default: all). */
 int cvr_set_path_range(cvr_ctx* ctx, uint64_t first, uint64_t count);
+/* Extension for multi-GPU strong scaling: restrict every launch to shard
+ * `rank` of `world` of the tile's work.  Launches in the pixel-block work
+ * order (whole samples of a tile whose sides are multiples of 8) take the
+ * tile's 8x8 pixel blocks rank, rank + world, ... with all their samples, so
+ * every shard sees the whole image and costs about the same; other launches
+ * take a contiguous 1/world share of their path ids.  Either way the shards of
+ * ranks 0..world-1 partition the launch's path ids, and the RNG stays bound
+ * to the path id, so their summed images equal the unsharded render up to
+ * fp32 summation order.  (0, 1) = no shard (default). */
+int cvr_set_block_shard(cvr_ctx* ctx, uint32_t rank, uint32_t world);
 /* RNG seed base (RegenerationVolPTsk_kernel.cuh:18 `seed`); path p uses
  * curand_init(seed + p). */
 int cvr_set_seed(cvr_ctx* ctx, uint32_t seed);

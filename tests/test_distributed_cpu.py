@@ -223,3 +223,69 @@ def test_three_rank_gloo_tile_path_sharding_equals_tile_loop(tmp_path, kernel):
     img, ref = np.nan_to_num(img[..., :3]), np.nan_to_num(ref[..., :3])
     bound = 2 * 3 * ITERS * 2.0 ** -24 * np.maximum(np.abs(img), np.abs(ref)) + 1e-30
     assert (np.abs(img - ref) <= bound).all()
+
+
+# ------------------------------------------------------------ block shards ----
+@pytest.mark.parametrize("tw,th,samples,world", [(24, 16, 3, 2), (24, 16, 3, 3), (64, 8, 2, 8), (8, 8, 1, 4)])
+def test_block_shards_partition_path_ids(tw, th, samples, world):
+    """cvr_set_block_shard's shards (blocks r, r+world, ..., every sample)
+    partition the launch's path ids, and no shard exceeds another by more
+    than one block of every sample."""
+    from cudavolumerenderer_amd.distributed import block_shard_path_ids
+    ids = [block_shard_path_ids(tw, th, samples, r, world) for r in range(world)]
+    allids = np.sort(np.concatenate(ids))
+    assert np.array_equal(allids, np.arange(tw * th * samples))
+    sizes = [len(i) for i in ids]
+    assert max(sizes) - min(sizes) <= 64 * samples
+    with pytest.raises(ValueError):
+        block_shard_path_ids(12, 8, 1, 0, 2)
+
+
+def _block_worker(rank, world, port, outdir):
+    from cudavolumerenderer_amd.distributed import HostImage, block_shard_path_ids, reduce_to_host
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        orc, L = _scene_and_launch()
+        n = W * H * 4
+        host = HostImage(torch, dist, n, rank, world, tag=f"test_{port}", pin=False)
+        acc_flat = torch.zeros(host.chunk * world, dtype=torch.float32)
+        acc = acc_flat[:n].view(-1, 4).numpy()
+        ids = block_shard_path_ids(W, H, ITERS, rank, world)
+        steps = 0
+        for start in ids[::8]:  # one 8-pixel row of a block: 8 consecutive path ids
+            rec = orc.trace_paths(L, int(start), 8)
+            steps += int(rec["n_steps"].sum())
+            esc = rec[(rec["flags"] & 1) != 0]
+            np.add.at(acc[:, :3], esc["image_id"], esc["T"])
+            acc[esc["image_id"], 3] = 1.0
+        part = torch.empty(host.chunk, dtype=torch.float32)
+        reduce_to_host(acc_flat, part, host, float(ITERS), dist)  # bench.py's end of a render
+        counts = torch.tensor([steps, len(ids)], dtype=torch.int64)
+        dist.all_reduce(counts)
+        dist.barrier()
+        if rank == 0:
+            np.save(os.path.join(outdir, "img.npy"), host.flat[:n].numpy().reshape(H, W, 4).copy())
+            np.save(os.path.join(outdir, "counts.npy"), counts.numpy())
+        host.close(dist)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_block_shard_gloo_render_equals_single(tmp_path, world):
+    """bench.py's default multi-GPU step on CPU: every rank renders its block
+    shard (the oracle stands in for k_wpool), one reduce-scatter sums the
+    framebuffers, every rank normalises and writes its slice into the shared
+    host image; the image equals the 1-rank render /iterations."""
+    mp.start_processes(_block_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="fork")
+    img = np.load(tmp_path / "img.npy")
+    counts = np.load(tmp_path / "counts.npy")
+    orc, L = _scene_and_launch()
+    ref, st = orc.render(L, 0, W * H * ITERS, nthreads=2)
+    ref = ref / np.float32(ITERS)
+    assert tuple(counts) == (st.steps, st.paths)
+    bound = 2 * ITERS * 2.0 ** -24 * np.maximum(np.abs(img), np.abs(ref)) + 1e-30
+    assert (np.abs(img[..., :3] - ref[..., :3]) <= bound[..., :3]).all()
+    assert img[..., :3].max() > 0

@@ -429,3 +429,39 @@ def test_wave_pool_scheduler_matches_persistent(cvr, scenes, scene_key):
         key = (st.paths, st.segments, st.steps, st.density, st.albedo, st.escaped, st.fetches)
         assert key == key0, (batch, grid, chunk, order)
         assert_pixels_close(img, img0, 4)
+
+
+@pytest.mark.parametrize("kernel", ["regenerationSK", "streamingSK", "naiveSK"])
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_block_shards_sum_to_whole_render(cvr, scenes, kernel, world):
+    """cvr_set_block_shard (bench.py's strong-scaling shards): the world
+    shards of a launch render exactly its paths (counters add up) and their
+    framebuffers sum to the unsharded one; on a tile whose sides are not
+    multiples of 8 the shards are contiguous path ranges."""
+    scene = scenes["manix_small"]
+    for W, H in ((128, 96), (100, 60)):
+        iters = 3
+        whole, _, _ = make_ctx(cvr, scene, W, H, kernel, seed=3)
+        whole.set_resolution(W, H)
+        whole.set_iterations(iters)
+        whole.clear_output()
+        whole.launch_render()
+        s0 = whole.stats()
+        full = whole.copy_output(W, H)
+        total = np.zeros_like(full)
+        acc = dict(paths=0, steps=0, density=0, albedo=0, escaped=0, segments=0)
+        for r in range(world):
+            ctx, _, _ = make_ctx(cvr, scene, W, H, kernel, seed=3)
+            ctx.set_resolution(W, H)
+            ctx.set_iterations(iters)
+            ctx.set_block_shard(r, world)
+            ctx.clear_output()
+            ctx.launch_render()
+            st = ctx.stats()
+            for k in acc:
+                acc[k] += getattr(st, k)
+            total[..., :3] += ctx.copy_output(W, H)[..., :3]
+            ctx.close()
+        for k in acc:
+            assert acc[k] == getattr(s0, k), (W, k)
+        assert_pixels_close(total[..., :3], full[..., :3], iters)

@@ -26,6 +26,7 @@ for step in "$@"; do
     pytest) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q -x --timeout 900 -p no:cacheprovider ;;
     pytestall) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q --timeout 900 -p no:cacheprovider ;;
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
+    benchd) run benchd 600 python3 bench.py --steps 20 --warmup 5 ;;
     bench_c3) run bench_c3 600 python3 bench.py --steps 10 --warmup 2 --scene hetvol ;;
     bench_c4) run bench_c4 600 python3 bench.py --steps 3 --warmup 1 --shard tiles --resolution 2048 2048 --iterations 256 --no-cpu-baseline ;;
     bench_c5) run bench_c5 600 python3 bench.py --steps 5 --warmup 1 --scene cloud ;;
@@ -47,8 +48,8 @@ for step in "$@"; do
     pmc_e) run pmc_e 90 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES --kernel-trace -d "$OUT/pmc_e" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     # per-scene profiles: prof:SCENE, pmcf:SCENE (FETCH_SIZE), pmcw:SCENE (WRITE_SIZE)
     prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline ;;
-    pmcf:*) sc=${step#pmcf:}; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
-    pmcw:*) sc=${step#pmcw:}; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmcf:*) sc=${step#pmcf:}; mkdir -p "$OUT/pmcf_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcf_$sc/libcvr.sha256"; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmcw:*) sc=${step#pmcw:}; mkdir -p "$OUT/pmcw_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcw_$sc/libcvr.sha256"; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
     # A/B of experiment builds: ab:SCENE:ROUNDS:variant1,variant2,...
     ab:*) IFS=: read -r _ sc rounds vs <<< "$step"; run ab_$sc 400 bash tools/ab.sh $sc $rounds ${vs//,/ } ;;
     *) echo "unknown step $step" ;;

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Per-launch HBM traffic of the dominant kernel from separate rocprofv3 --pmc
-passes (FETCH_SIZE, WRITE_SIZE), corrected as MI355X_MICROARCH.md §HBM says:
+passes (FETCH_SIZE, WRITE_SIZE), corrected as MI355X_MICROARCH.md §HBM says
+(stamped with the sha256 of the libcvr.so the passes ran, which bench.py
+checks before it reports the traffic):
 FETCH_SIZE (KB) counts 128-B requests as 64 B on gfx950 -> x2; WRITE_SIZE (KB)
 is exact for 16-B stores / f32 atomics.  Writes profiles/traffic.json.
 
@@ -31,11 +33,17 @@ def main():
     w = write[1:] if len(write) > 1 else write
     fb = 2.0 * 1024.0 * sum(f) / len(f)
     wb = 1024.0 * sum(w) / len(w)
+    shas = set()
+    for d in (fdir, wdir):
+        p = os.path.join(d, "libcvr.sha256")
+        shas.add(open(p).read().split()[0] if os.path.exists(p) else None)
+    if len(shas) != 1 or None in shas:
+        sys.exit(f"libcvr.sha256 missing or different in {fdir} / {wdir}: {shas}")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = os.path.join(root, "profiles", "traffic.json")
     data = json.load(open(out)) if os.path.exists(out) else {}
     data[key] = {"fetch_bytes": fb, "write_bytes": wb, "bytes_per_launch": fb + wb,
-                 "dispatches": len(f), "kernel": kname,
+                 "dispatches": len(f), "kernel": kname, "libcvr_sha256": shas.pop(),
                  "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE in separate passes; "
                            "FETCH_SIZE x2 (gfx950 counts 128-B requests as 64 B), KB x1024; "
                            "includes Infinity-Cache hits (memory-side of L2)"}
