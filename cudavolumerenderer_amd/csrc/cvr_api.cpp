@@ -112,6 +112,7 @@ struct cvr_ctx {
   uint32_t ev_thresh = 56;
   uint32_t grid_override = 0;
   int scatter_eps = -1;
+  int rng_binding = 0;  // CVR_OPT_RNG_BINDING
 
   int cu_count = 0;
   int persistent_grid = 0;
@@ -216,7 +217,8 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   const uint64_t P0 = (uint64_t)(uint32_t)((float)c->tile_w * (float)c->tile_h);
   // the persistent schedulers take work units through unit_to_path (pixel-block order); naiveSK/MK
   // and the wavefront pair map launch index -> path id directly
-  const bool queued = c->kernel != CVR_KERNEL_NAIVE_SK && c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1;
+  const bool queued = c->kernel != CVR_KERNEL_NAIVE_SK && c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 &&
+                      c->rng_binding == 0;
   const bool block_order = queued && c->order && P0 && first % P0 == 0 && count % P0 == 0 && count > 0 &&
                            c->tile_w % 8 == 0 && c->tile_h % 8 == 0;
   if (shard_world > 1 && !block_order) {  // no block order: a contiguous share of the path ids
@@ -857,6 +859,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       // takes effect at the next cvr_set_medium
       c->use_cells = v != 0;
       return CVR_OK;
+    case CVR_OPT_RNG_BINDING:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "rng binding must be 0 (path) or 1 (thread)");
+      c->rng_binding = (int)v;
+      return CVR_OK;
     case CVR_OPT_SCATTER_EPS:
       if (v < -1 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "scatter_eps must be -1, 0 or 1");
       c->scatter_eps = (int)v;
@@ -908,7 +914,16 @@ int cvr_launch_render(cvr_ctx* c) {
   HIP_TRY(c, hipEventRecord(c->ev_start, c->stream));
   c->last_iterations = 0;
   c->last_track_ms = c->last_events_ms = 0;
-  if (c->kernel == CVR_KERNEL_NAIVE_SK) {
+  if (c->rng_binding == 1) {
+    if (c->kernel != CVR_KERNEL_REGENERATION_SK)
+      return set_err(&c->err, CVR_ERR_UNSUPPORTED, "thread-bound RNG (CVR_OPT_RNG_BINDING 1) is regenerationSK only");
+    if (L.order) {  // one queue of path ids in order: the thread-bound kernel has no work bands
+      L.order = 0;
+      L.n_queues = 1;
+    }
+    const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 16u;
+    HIP_TRY(c, cvr::launch_regen_thread(c->m, L, eps, grid, c->stream));
+  } else if (c->kernel == CVR_KERNEL_NAIVE_SK) {
     HIP_TRY(c, cvr::launch_naive(c->m, L, eps, c->stream));
   } else if (c->kernel == CVR_KERNEL_NAIVE_MK) {
     HIP_TRY(c, cvr::launch_naive_mk(c->m, L, c->stream));

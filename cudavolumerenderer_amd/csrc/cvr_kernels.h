@@ -49,6 +49,10 @@ hipError_t pool_occupancy(bool scatter_eps, int* blocks_per_cu);
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
                         hipStream_t s);
 hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu);
+// regenerationSK with the RNG bound to the persistent thread (CVR_OPT_RNG_BINDING 1):
+// `grid` one-wave workgroups, path ids from the launch's single queue head.
+hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
+                               hipStream_t s);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);

@@ -161,6 +161,92 @@ __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, P
   if (n_fetch) atomicAdd(L.stats + STAT_FETCH, (unsigned long long)n_fetch);
 }
 
+// ------------------------------------------- thread-bound regenerationSK ---
+// RegenerationVolPTsk_kernel::d_render_single_thread_regeneration
+// (RegenerationVolPTsk_kernel.cuh:146-232) with the reference's RNG binding
+// (CVR_OPT_RNG_BINDING = 1): persistent thread tid draws every
+// path it takes from one stream, Rng(seed + tid); one loop iteration takes a
+// path if idle, runs one segment and the roulette, which also runs (one
+// draw) after an escape (:220-229); the isect lives across the thread's paths
+// (:155).  Idle lanes take consecutive path ids in lane order from one
+// wave-aggregated atomic, so a one-wave launch is deterministic (the oracle's
+// oracle_render_thread_bound); with more waves the path -> thread assignment
+// depends on timing, as in the reference.  Lanes whose queue ran dry stay in
+// the loop (idle) until the whole wave is done, so the wave's collectives
+// always see lane 0.
+template <bool kScatterEps>
+__global__ __launch_bounds__(64) void k_regen_thread(MediumParams m, LaunchParams L) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = blockIdx.x * 64u + lane;
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  PathState ps;
+  rng_init(ps.rng, (int32_t)(L.seed_base + tid));  // Rng(seed + tid): int, sign-extended (Q3)
+  ps.o = ps.d = ps.T = mk3(0, 0, 0);
+  ps.image_id = 0;
+  Isect is;
+  is.dist = 0.0f;
+  is.normal = mk3(0, 0, 0);
+  is.inside = false;
+  bool active = false, done = false;
+  uint32_t nseg = 0;
+  for (;;) {
+    // ---- regenerate (:160-180)
+    const unsigned long long need = __ballot(!active && !done);
+    if (need) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(L.queue, (unsigned int)__popcll(need));
+      base = __shfl(base, 0);
+      if (!active && !done) {
+        const uint32_t h =
+            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        if (h >= L.path_count) {
+          done = true;
+        } else {
+          const uint32_t path_id = L.path_first + h;
+          ps.image_id = path_id - fastdiv(path_id, L.div_tile_px) * L.tile_px;
+          camera_ray(L, ps);  // from the thread's stream
+          nseg = 0;
+          active = true;
+          ++c[STAT_PATHS];
+        }
+      }
+    }
+    if (__ballot(!done) == 0ull) break;
+    if (!active) continue;
+    if (L.max_segments && nseg >= L.max_segments) {  // safety cap, as the path-bound walk
+      ++c[STAT_TRUNCATED];
+      active = false;
+      continue;
+    }
+    ++nseg;
+    ++c[STAT_SEGMENTS];
+    if (!aabb_intersect(m, ps.o, ps.d, is)) {
+      splat(L, ps);
+      ++c[STAT_ESCAPED];
+      active = false;
+      (void)roulette(ps);  // the reference's roulette block draws after an escape too
+      continue;
+    }
+    float t = 0.0f;
+    bool collided = false;
+    if (is.inside) {
+      int r;
+      do {
+        r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
+      } while (r == 0);
+      collided = t < is.dist;
+    }
+    if (!collided) {
+      boundary_event(m, ps, is);
+    } else {
+      scatter_event<kScatterEps>(m, ps, t);
+      ++c[STAT_ALBEDO];
+    }
+    if (!roulette(ps)) active = false;
+  }
+  flush_stats(L, c);
+}
+
 // ----------------------------------------------------- image transfer -----
 // Intended semantics of HostImageBufferTansferDelegate::transfer
 // (ImageBufferTransfer.cu:61-78, fixed per SURVEY Q10): image[off + p] =
@@ -308,6 +394,16 @@ hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatt
     hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(256), 0, s, m, L, rec);
   else
     hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(256), 0, s, m, L, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
+                               hipStream_t s) {
+  if (L.path_count == 0 || grid == 0) return hipSuccess;
+  if (scatter_eps)
+    hipLaunchKernelGGL(k_regen_thread<true>, dim3(grid), dim3(64), 0, s, m, L);
+  else
+    hipLaunchKernelGGL(k_regen_thread<false>, dim3(grid), dim3(64), 0, s, m, L);
   return hipGetLastError();
 }
 

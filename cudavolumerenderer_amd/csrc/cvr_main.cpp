@@ -27,7 +27,7 @@ namespace {
 
 struct Options {
   std::string scene_file, scene_type = "Auto", algorithm = "cudaVolPath", kernel = "regenerationSK";
-  std::string output, synthetic;
+  std::string output, synthetic, rng_binding = "path";
   bool interactive = true, unified = false;
   unsigned trials = 1, iterations = 20, device = 0, seed = 0;
   std::vector<unsigned> tiles{1, 1}, resolution{1024, 1024};
@@ -53,7 +53,9 @@ void usage() {
       "  -r [ --resolution ] arg (=1024 1024)\n"
       "Extensions:\n"
       "  --synthetic bucky|manix|hetvol|cloud  use a built-in proxy scene\n"
-      "  --device N, --seed S\n");
+      "  --device N, --seed S\n"
+      "  --rng-binding path|thread (=path)  regenerationSK: thread = the reference's Rng(seed + tid)\n"
+      "                                     per persistent thread (non-deterministic, SURVEY Q2)\n");
 }
 
 bool is_flag(const char* a) { return a[0] == '-' && !(a[1] >= '0' && a[1] <= '9'); }
@@ -90,6 +92,7 @@ int parse(int argc, char** argv, Options& o) {
     else if (a == "-r" || a == "--resolution") multi(o.resolution);
     else if (a == "--synthetic") o.synthetic = need("synthetic");
     else if (a == "--device") o.device = (unsigned)strtoul(need("device").c_str(), nullptr, 10);
+    else if (a == "--rng-binding") o.rng_binding = need("rng-binding");
     else if (a == "--seed") o.seed = (unsigned)strtoul(need("seed").c_str(), nullptr, 10);
     else if (!is_flag(a.c_str()) && o.scene_file.empty()) o.scene_file = a;  // positional
     else {
@@ -183,6 +186,14 @@ int main(int argc, char** argv) {
       return 1;
     }
     cvr_set_seed(ctx, o.seed);
+    if (o.rng_binding != "path" && o.rng_binding != "thread") {
+      fprintf(stderr, "[ConfigParser] Error: --rng-binding must be path or thread\n");
+      return 2;
+    }
+    if (o.rng_binding == "thread" && (r = cvr_set_option(ctx, CVR_OPT_RNG_BINDING, 1)) != CVR_OK) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
+      return 1;
+    }
     if (!sparse && (r = cvr_set_medium(ctx, &md)) == CVR_ERR_UNSUPPORTED) {
       printf("[Scene] dense grid rejected (%s); using the sparse leaf upload\n", cvr_last_error(ctx));
       if ((r = cvr_scene_sparse_medium(scene, &sd)) != CVR_OK) return 1;

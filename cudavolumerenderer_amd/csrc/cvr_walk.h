@@ -638,9 +638,15 @@ struct PathState {
   V3 o, d, T;
   uint32_t image_id;
 };
+// Camera ray of pixel ps.image_id drawn from ps.rng (indexToCameraRay,
+// Utilities.cuh:180-213).
+CVR_DEV void camera_ray(const LaunchParams& L, PathState& ps);
 CVR_DEV void path_begin(const LaunchParams& L, uint32_t path_id, PathState& ps) {
   ps.image_id = path_id - fastdiv(path_id, L.div_tile_px) * L.tile_px;  // path_id % tile_px
   rng_init(ps.rng, (int32_t)(L.seed_base + path_id));
+  camera_ray(L, ps);
+}
+CVR_DEV void camera_ray(const LaunchParams& L, PathState& ps) {
   const float px = (float)(ps.image_id - fastdiv(ps.image_id, L.div_tile_w) * L.tile_w) + (float)L.off[0];
   const float py = det_floorf((float)ps.image_id / L.tile_res[0]) + (float)L.off[1];
   const float r0 = rng_float(ps.rng);

@@ -24,7 +24,9 @@
  *     that the HIP kernels can be bit-exact with this oracle per path;
  *   - FMA contraction is explicit (det_fmaf) at the three hot-loop sites
  *     listed in DESIGN.md, everything else is uncontracted IEEE;
- *   - RNG is bound to path_id for every scheduler.
+ *   - RNG is bound to path_id for every scheduler, except in
+ *     oracle_render_thread_bound, which restates regenerationSK's own
+ *     Rng(seed + tid) binding for lockstep threads (CVR_OPT_RNG_BINDING 1).
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -700,6 +702,128 @@ EXPORT int oracle_render(const oracle_medium* m, const oracle_launch* L, uint64_
   if (stats) *stats = st;
   free(jobs);
   free(th);
+  return 0;
+}
+
+/* ---------------------------------------- thread-bound regenerationSK -- */
+/* RegenerationVolPTsk_kernel::d_render_single_thread_regeneration
+ * (RegenerationVolPTsk_kernel.cuh:146-232) with the RNG bound to the
+ * persistent THREAD, not the path (CVR_OPT_RNG_BINDING = 1):
+ *   - thread tid owns one stream, Rng(seed + tid) (:156), for every path it
+ *     takes;
+ *   - one loop iteration = [take a path if idle] + one segment + roulette;
+ *     the roulette block runs after an escape too (:220-229), so an escaping
+ *     path draws one more number from the thread's stream;
+ *   - the SimpleIsect lives across the thread's paths (:155): a segment whose
+ *     distance matches no box plane keeps the previous path's normal.
+ * The reference takes path ids with one atomicAdd per idle thread, in an
+ * order the hardware picks.  Restated here for `n_threads` threads advancing
+ * in lockstep, idle threads taking consecutive ids in thread order at the top
+ * of each iteration: the order a single 64-lane wave produces with one
+ * wave-aggregated atomic (k_regen_thread launched as one wave), so that
+ * launch is deterministic and comparable path by path.  Path ids are
+ * first + [0, count); `out` is the tile accumulator (float4 per pixel). */
+typedef struct {
+  xorwow_t rng;
+  isect_t is;
+  f3 o, d, T;
+  uint32_t image_id, nseg;
+  int active, done;
+} tb_thread_t;
+
+EXPORT int oracle_render_thread_bound(const oracle_medium* m, const oracle_launch* L, uint32_t n_threads,
+                                      uint32_t first, uint32_t count, float* out, oracle_stats* stats) {
+  if (n_threads == 0) return -1;
+  tb_thread_t* th = (tb_thread_t*)calloc(n_threads, sizeof(tb_thread_t));
+  if (!th) return -1;
+  oracle_stats st;
+  memset(&st, 0, sizeof(st));
+  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
+  for (uint32_t t = 0; t < n_threads; ++t) {
+    rng_init(&th[t].rng, (int32_t)(L->seed_base + t)); /* Rng(seed + tid): int, sign-extended (Q3) */
+    th[t].is.dist = 0.0f;
+    th[t].is.normal = mk3(0, 0, 0);
+    th[t].is.inside = 0;
+  }
+  uint32_t head = 0, live = n_threads;
+  while (live) {
+    /* regenerate (:160-180): idle threads take ids in thread order */
+    for (uint32_t t = 0; t < n_threads; ++t) {
+      tb_thread_t* p = &th[t];
+      if (p->done || p->active) continue;
+      if (head >= count) {
+        p->done = 1;
+        --live;
+        continue;
+      }
+      const uint32_t path_id = first + head++;
+      p->image_id = path_id % tile_px;
+      float px = (float)(p->image_id % (uint32_t)L->tile_res[0]) + (float)L->offset[0];
+      float py = det_floorf((float)p->image_id / L->tile_res[0]) + (float)L->offset[1];
+      camera_ray(L, px, py, &p->rng, &p->o, &p->d);
+      p->T = mk3(1.0f, 1.0f, 1.0f);
+      p->nseg = 0;
+      p->active = 1;
+      st.paths++;
+    }
+    for (uint32_t t = 0; t < n_threads; ++t) {
+      tb_thread_t* p = &th[t];
+      if (!p->active) continue;
+      if (L->max_segments && p->nseg >= L->max_segments) { /* safety cap, as the path-bound walk */
+        st.truncated++;
+        p->active = 0;
+        continue;
+      }
+      p->nseg++;
+      st.segments++;
+      if (!aabb_intersect(m, p->o, p->d, &p->is)) {
+        float* px = out + 4 * (size_t)p->image_id; /* atomicVectorAdd(T * Le), Le = 1 */
+        px[0] += p->T.x;
+        px[1] += p->T.y;
+        px[2] += p->T.z;
+        px[3] = 1.0f;
+        st.escaped++;
+        p->active = 0;
+      } else {
+        float sampled = 0.0f;
+        int collided = 0;
+        uint32_t ns = 0, nd = 0;
+        if (p->is.inside) {
+          sampled = woodcock(m, p->o, p->d, p->is.dist, &p->rng, &ns, &nd);
+          collided = sampled < p->is.dist;
+        }
+        st.steps += ns;
+        st.density += nd;
+        if (!collided) {
+          frame_t fr = frame_from_z(p->is.normal);
+          f3 dir = frame_to_local(&fr, normalize3(neg3(p->d)));
+          p->o = add3(p->o, scl3(p->d, p->is.dist));
+          float weight = 1.0f;
+          if (ggx_sample(m, dir, &p->rng, &p->d, &weight)) {
+            p->T = scl3(p->T, weight);
+            p->d = frame_to_world(&fr, p->d);
+            p->o = add3(p->o, scl3(p->d, EPS));
+          }
+        } else {
+          p->o = add3(p->o, scl3(p->d, sampled)); /* no -eps (:212) */
+          f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
+          f3 bmax = mk3(m->box_max[0], m->box_max[1], m->box_max[2]);
+          f3 a = albedo_lookup(m, div3(sub3(p->o, bmin), sub3(bmax, bmin)));
+          st.albedo++;
+          p->T = mul3(p->T, a);
+          float e1 = rng_float(&p->rng);
+          float e2 = rng_float(&p->rng);
+          p->d = hg_sample(p->d, m->g, e1, e2);
+        }
+      }
+      /* roulette (:220-229): runs whether or not the path escaped */
+      float q = det_fminf(1.0f, det_fmaxf(det_fmaxf(p->T.x, p->T.y), p->T.z));
+      if (rng_float(&p->rng) > q) p->active = 0;
+      p->T = mk3(p->T.x / q, p->T.y / q, p->T.z / q);
+    }
+  }
+  free(th);
+  if (stats) *stats = st;
   return 0;
 }
 

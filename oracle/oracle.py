@@ -67,6 +67,9 @@ def load():
                                   C.c_uint64, C.c_uint64, C.POINTER(C.c_float), C.c_int,
                                   C.POINTER(OracleStats)]
     lib.oracle_render.restype = C.c_int
+    lib.oracle_render_thread_bound.argtypes = [C.POINTER(OracleMedium), C.POINTER(OracleLaunch), C.c_uint32,
+                                               C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.POINTER(OracleStats)]
+    lib.oracle_render_thread_bound.restype = C.c_int
     lib.oracle_rng_stream.argtypes = [C.c_int32, C.c_uint32, P, P]
     lib.oracle_rng_state.argtypes = [C.c_int32, P]
     lib.oracle_density.argtypes = [C.POINTER(OracleMedium), P]
@@ -163,6 +166,18 @@ class Oracle:
         st = OracleStats()
         rc = self.lib.oracle_render(C.byref(self.m), C.byref(L), first, stride, count,
                                     out.ctypes.data_as(C.POINTER(C.c_float)), nthreads, C.byref(st))
+        assert rc == 0
+        return out, st
+
+    def render_thread_bound(self, L: OracleLaunch, n_threads: int, first: int, count: int):
+        """regenerationSK with the RNG bound to the thread: n_threads
+        lockstep threads, Rng(seed + tid) each (cvr_oracle.c
+        oracle_render_thread_bound).  Returns (tile accumulator, stats)."""
+        w, h = int(L.tile_res[0]), int(L.tile_res[1])
+        out = np.zeros((h, w, 4), np.float32)
+        st = OracleStats()
+        rc = self.lib.oracle_render_thread_bound(C.byref(self.m), C.byref(L), n_threads, first, count,
+                                                 out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st))
         assert rc == 0
         return out, st
 

@@ -1,0 +1,130 @@
+"""CVR_OPT_RNG_BINDING = 1: regenerationSK with the reference's thread-bound
+RNG (RegenerationVolPTsk_kernel.cuh:146-232): Rng(seed + tid) per
+persistent thread, a roulette draw after an escape, the isect kept across a
+thread's paths.
+
+The oracle restates it for lockstep threads taking path ids in thread order
+(oracle_render_thread_bound); a one-wave launch of k_regen_thread produces
+exactly that order, so it is compared with the oracle pixel by pixel and
+counter by counter.  Larger launches assign paths to threads by timing (as the
+reference does): checked for completeness and against the path-bound image
+statistically.
+"""
+import numpy as np
+import pytest
+
+from parity_util import NTHREADS, assert_pixels_close
+
+
+def _bucky_oracle(cvr, oracle_mod):
+    s = cvr.Scene.synthetic("bucky")
+    return s, oracle_mod.Oracle.from_medium_desc(s.medium, s.density, s.albedo)
+
+
+@pytest.mark.parametrize("seed", [0, 77])
+def test_oracle_thread_bound_with_a_thread_per_path_is_path_bound(cvr, oracle_mod, seed):
+    """With at least as many threads as paths every thread takes one path at
+    the first iteration, path i on thread i, so Rng(seed + tid) is the
+    path-bound stream: the thread-bound restatement equals the path-bound
+    regenerationSK walk (the extra roulette draw after an escape and the
+    carried isect cannot show)."""
+    s, orc = _bucky_oracle(cvr, oracle_mod)
+    W = H = 32
+    n = W * H * 2
+    iv, r2v = cvr.default_camera(W, H)
+    L = orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 2, seed)
+    a, sa = orc.render_thread_bound(L, n, 0, n)
+    b, sb = orc.render(L, 0, n, nthreads=NTHREADS)
+    assert sa.as_dict() == sb.as_dict()
+    assert_pixels_close(a, b, 2)
+
+
+def test_oracle_thread_bound_differs_from_path_bound_with_few_threads(cvr, oracle_mod):
+    """With 64 threads each thread walks many paths from one stream: the
+    image differs from the path-bound one (same paths rendered, other random
+    numbers), the path count and the pixel coverage do not."""
+    s, orc = _bucky_oracle(cvr, oracle_mod)
+    W = H = 32
+    n = W * H * 2
+    iv, r2v = cvr.default_camera(W, H)
+    L = orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 2, 0)
+    a, sa = orc.render_thread_bound(L, 64, 0, n)
+    b, sb = orc.render(L, 0, n, nthreads=NTHREADS)
+    assert sa.paths == sb.paths == n and sa.truncated == 0
+    assert sa.steps != sb.steps
+    assert not np.array_equal(a, b)
+    assert abs(a[..., :3].mean() - b[..., :3].mean()) < 0.1 * b[..., :3].mean()
+
+
+def _ctx(cvr, scene, W, H, grid):
+    ctx = cvr.Context(0, "regenerationSK")
+    ctx.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(W, H)
+    ctx.set_camera(iv, r2v, (W, H))
+    ctx.set_option(cvr.OPT_RNG_BINDING, 1)
+    if grid:
+        ctx.set_option(cvr.OPT_GRID, grid)
+    ctx.init()
+    return ctx, iv, r2v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene_name,seed,tiles", [("bucky", 0, (1, 1)), ("hetvol", 5, (1, 1)), ("bucky", 3, (2, 2))])
+def test_one_wave_thread_bound_launch_matches_oracle(cvr, oracle_mod, scene_name, seed, tiles):
+    s = cvr.Scene.synthetic(scene_name)
+    orc = oracle_mod.Oracle.from_medium_desc(s.medium, s.density, s.albedo)
+    W = H = 48
+    iters = 3
+    ctx, iv, r2v = _ctx(cvr, s, W, H, grid=1)
+    ctx.set_seed(seed)
+    img, st = ctx.render_image(W, H, tiles, iters)
+    tw, th = W // tiles[0], H // tiles[1]
+    n = tw * th * iters
+    ref = np.zeros((H, W, 4), np.float32)
+    tot = dict(paths=0, segments=0, steps=0, density=0, albedo=0, escaped=0)
+    for k in range(tiles[0] * tiles[1]):
+        ox, oy = tw * (k % tiles[0]), th * (k // tiles[0])
+        L = orc.launch(iv, r2v, (W, H), (tw, th), (ox, oy), 2, (seed + k * n) & 0xFFFFFFFF)
+        tile, rst = orc.render_thread_bound(L, 64, 0, n)
+        ref[oy:oy + th, ox:ox + tw] = tile / np.float32(iters)
+        for key in tot:
+            tot[key] += getattr(rst, key)
+    for key, v in tot.items():
+        assert getattr(st, key) == v, key
+    assert_pixels_close(img, ref, iters, f"thread-bound {scene_name}")
+    assert st.albedo > 0
+
+
+@pytest.mark.gpu
+def test_full_grid_thread_bound_renders_every_path(cvr):
+    """The default grid (16 waves per CU): every path is rendered exactly
+    once and the image agrees with the path-bound render in the mean (the
+    thread-bound streams are other random numbers, so only statistically)."""
+    s = cvr.Scene.synthetic("manix", 0, (64, 58, 64))
+    W = H = 128
+    iters = 16
+    tb, _, _ = _ctx(cvr, s, W, H, grid=0)
+    img, st = tb.render_image(W, H, (1, 1), iters)
+    assert st.paths == W * H * iters and st.truncated == 0
+    pb = cvr.Context(0, "regenerationSK")
+    pb.set_medium(s.medium)
+    iv, r2v = cvr.default_camera(W, H)
+    pb.set_camera(iv, r2v, (W, H))
+    pb.init()
+    ref, sr = pb.render_image(W, H, (1, 1), iters)
+    a, b = np.nanmean(img[..., :3]), np.nanmean(ref[..., :3])
+    assert abs(a - b) < 0.02 * b, (a, b)
+    assert abs(st.steps - sr.steps) < 0.02 * sr.steps
+
+
+@pytest.mark.gpu
+def test_thread_bound_is_regeneration_only(cvr):
+    s = cvr.Scene.synthetic("bucky")
+    ctx = cvr.Context(0, "naiveSK")
+    ctx.set_medium(s.medium)
+    iv, r2v = cvr.default_camera(32, 32)
+    ctx.set_camera(iv, r2v, (32, 32))
+    ctx.set_option(cvr.OPT_RNG_BINDING, 1)
+    with pytest.raises(cvr.CvrError) as e:
+        ctx.render_image(32, 32, (1, 1), 1)
+    assert "regenerationSK" in str(e.value)
