@@ -103,6 +103,8 @@ struct cvr_ctx {
   bool external_out = false;
 
   unsigned char* d_work = nullptr;  // queue heads + stats counters (kWork* layout)
+  float4* d_pool_T = nullptr;       // wave-pool scheduler: event-only slot part (LaunchParams::pool_T)
+  size_t pool_T_n = 0;
   uint32_t n_queues = 8;            // work-order bands (one per XCD)
   int order = 1;                    // 1: pixel-block/sample-inner order when the launch allows it
 
@@ -118,8 +120,10 @@ struct cvr_ctx {
   int persistent_grid = 0;
   int pool_grid = 0;
   uint32_t pool_tail = 16;
-  int wpool_grid = 0;
-  int wpool_waves = 4;  // wave-pool register/LDS budget: 4 or 5 waves per SIMD
+  int wpool_grid = 0, wpool_grid_sparse = 0;
+  // wave-pool register/LDS budget in waves per SIMD (CVR_OPT_WAVES: 3, 4, 5);
+  // 0 = per medium: 5 dense (split slots), 4 sparse
+  int wpool_waves = 0;
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
@@ -178,6 +182,11 @@ int scheduler_for(const cvr_ctx* c) {
 bool scatter_eps_for(const cvr_ctx* c) {
   if (c->scatter_eps >= 0) return c->scatter_eps != 0;
   return c->kernel != CVR_KERNEL_REGENERATION_SK;
+}
+
+int wpool_waves_for(const cvr_ctx* c, bool sparse) {
+  if (c->wpool_waves) return c->wpool_waves;
+  return sparse ? 4 : 5;
 }
 
 int ensure_device(cvr_ctx* c) {
@@ -306,9 +315,12 @@ int do_init(cvr_ctx* c) {
   if (pbpc < 1) pbpc = 1;
   c->pool_grid = pbpc * c->cu_count;
   int wbpc = 0;
-  HIP_TRY(c, cvr::wpool_occupancy(scatter_eps_for(c), c->wpool_waves, &wbpc));
+  HIP_TRY(c, cvr::wpool_occupancy(scatter_eps_for(c), wpool_waves_for(c, false), false, &wbpc));
   if (wbpc < 1) wbpc = 1;
   c->wpool_grid = wbpc * c->cu_count;
+  HIP_TRY(c, cvr::wpool_occupancy(scatter_eps_for(c), wpool_waves_for(c, true), true, &wbpc));
+  if (wbpc < 1) wbpc = 1;
+  c->wpool_grid_sparse = wbpc * c->cu_count;
   int tbpc = 0;
   HIP_TRY(c, cvr::wf_track_occupancy(&tbpc));
   if (tbpc < 1) tbpc = 1;
@@ -484,6 +496,7 @@ int cvr_destroy(cvr_ctx* c) {
   free_sparse(c);
   if (c->d_out_owned) (void)hipFree(c->d_out_owned);
   if (c->d_work) (void)hipFree(c->d_work);
+  if (c->d_pool_T) (void)hipFree(c->d_pool_T);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -903,7 +916,8 @@ int cvr_launch_render(cvr_ctx* c) {
   // (waves: at most 4 per block of any scheduler).
   const uint64_t waves_max =
       4ull * (c->grid_override ? c->grid_override
-                               : (uint64_t)std::max({c->persistent_grid, c->pool_grid, c->wpool_grid}));
+                               : (uint64_t)std::max({c->persistent_grid, c->pool_grid, c->wpool_grid,
+                                                      c->wpool_grid_sparse}));
   uint64_t units_max = L.order ? 0 : count;
   for (uint32_t q = 0; L.order && q < L.n_queues; ++q)
     units_max = std::max<uint64_t>(units_max, (uint64_t)(L.qbeg[q + 1] - L.qbeg[q]) * 64u * L.samples);
@@ -934,8 +948,20 @@ int cvr_launch_render(cvr_ctx* c) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->pool_grid;
     HIP_TRY(c, cvr::launch_pool(c->m, L, eps, grid, c->stream));
   } else if (scheduler_for(c) == 3) {
-    const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->wpool_grid;
-    HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, c->wpool_waves, grid, c->stream));
+    const bool sparse = c->m.leaves != nullptr;
+    const int waves = wpool_waves_for(c, sparse);
+    const uint32_t grid =
+        c->grid_override ? c->grid_override : (uint32_t)(sparse ? c->wpool_grid_sparse : c->wpool_grid);
+    const size_t need = (size_t)grid * cvr::wpool_slots(waves, sparse);
+    if (need > c->pool_T_n) {
+      if (c->d_pool_T) (void)hipFree(c->d_pool_T);
+      c->d_pool_T = nullptr;
+      c->pool_T_n = 0;
+      HIP_TRY(c, hipMalloc(&c->d_pool_T, need * sizeof(float4)));
+      c->pool_T_n = need;
+    }
+    L.pool_T = c->d_pool_T;
+    HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, waves, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }

@@ -48,7 +48,10 @@ hipError_t launch_pool(const MediumParams& m, const LaunchParams& L, bool scatte
 hipError_t pool_occupancy(bool scatter_eps, int* blocks_per_cu);
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
                         hipStream_t s);
-hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu);
+hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu);
+// Pool slots per wave of the wave-pool kernel instance (LaunchParams::pool_T
+// needs grid * slots float4).
+uint32_t wpool_slots(int waves, bool sparse);
 // regenerationSK with the RNG bound to the persistent thread (CVR_OPT_RNG_BINDING 1):
 // `grid` one-wave workgroups, path ids from the launch's single queue head.
 hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,

@@ -163,6 +163,7 @@ struct LaunchParams {
   float4* out;            // tile accumulator, tile_px float4
   unsigned int* queue;    // work-queue heads, one per 64-byte line (zeroed per launch)
   unsigned long long* stats;  // CVR_STAT_* counters (zeroed per launch)
+  float4* pool_T;         // wave-pool scheduler: event-only slot part, grid * slots float4 (cvr_api wpool_slots)
   uint32_t chunk;         // paths per wave dequeue
   uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
   uint32_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track
@@ -305,20 +306,28 @@ CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p) {
 }
 CVR_DEV V3 albedo_lookup(const MediumParams& m, V3 p) {
   const Tri t = tri_setup(m, p);
-  const float4 d000 = texel_albedo(m, t.xa, t.ya, t.za), d001 = texel_albedo(m, t.xb, t.ya, t.za);
-  const float4 d010 = texel_albedo(m, t.xa, t.yb, t.za), d011 = texel_albedo(m, t.xb, t.yb, t.za);
-  const float4 d100 = texel_albedo(m, t.xa, t.ya, t.zb), d101 = texel_albedo(m, t.xb, t.ya, t.zb);
-  const float4 d110 = texel_albedo(m, t.xa, t.yb, t.zb), d111 = texel_albedo(m, t.xb, t.yb, t.zb);
   const float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
-#define CVR_TRI(c)                                                                     \
-  lerpf(lerpf(lerpf(d000.c, d001.c, t.fx, _fx), lerpf(d010.c, d011.c, t.fx, _fx), t.fy, \
-              _fy),                                                                    \
-        lerpf(lerpf(d100.c, d101.c, t.fx, _fx), lerpf(d110.c, d111.c, t.fx, _fx), t.fy, \
-              _fy),                                                                    \
-        t.fz, _fz)
-  const V3 r = mk3(CVR_TRI(x), CVR_TRI(y), CVR_TRI(z));
-#undef CVR_TRI
-  return r;
+  // one z plane at a time (same operations as the 8-tap form: x, then y
+  // lerps per plane, then z), so at most 4 texels are live
+  V3 a, b;
+  {
+    const float4 d000 = texel_albedo(m, t.xa, t.ya, t.za), d001 = texel_albedo(m, t.xb, t.ya, t.za);
+    const float4 d010 = texel_albedo(m, t.xa, t.yb, t.za), d011 = texel_albedo(m, t.xb, t.yb, t.za);
+    a = mk3(lerpf(lerpf(d000.x, d001.x, t.fx, _fx), lerpf(d010.x, d011.x, t.fx, _fx), t.fy, _fy),
+            lerpf(lerpf(d000.y, d001.y, t.fx, _fx), lerpf(d010.y, d011.y, t.fx, _fx), t.fy, _fy),
+            lerpf(lerpf(d000.z, d001.z, t.fx, _fx), lerpf(d010.z, d011.z, t.fx, _fx), t.fy, _fy));
+  }
+  // keep the second plane's loads after the first plane's lerps (otherwise
+  // the scheduler issues all 8 loads first: 32 live VGPRs at the peak)
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const float4 d100 = texel_albedo(m, t.xa, t.ya, t.zb), d101 = texel_albedo(m, t.xb, t.ya, t.zb);
+    const float4 d110 = texel_albedo(m, t.xa, t.yb, t.zb), d111 = texel_albedo(m, t.xb, t.yb, t.zb);
+    b = mk3(lerpf(lerpf(d100.x, d101.x, t.fx, _fx), lerpf(d110.x, d111.x, t.fx, _fx), t.fy, _fy),
+            lerpf(lerpf(d100.y, d101.y, t.fx, _fx), lerpf(d110.y, d111.y, t.fx, _fx), t.fy, _fy),
+            lerpf(lerpf(d100.z, d101.z, t.fx, _fx), lerpf(d110.z, d111.z, t.fx, _fx), t.fy, _fy));
+  }
+  return mk3(lerpf(a.x, b.x, t.fz, _fz), lerpf(a.y, b.y, t.fz, _fz), lerpf(a.z, b.z, t.fz, _fz));
 }
 
 // ---------------------------------------------------------------- AABB ----

@@ -49,35 +49,60 @@ namespace cvr {
 
 namespace {
 
+// An SGPR value the compiler may not look through: computations that depend on
+// it stay where they are written (inside the event batch) instead of being
+// hoisted to the kernel prologue and held in VGPRs for the whole kernel.
+__device__ __forceinline__ float opaque_s(float x) {
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
 // Paths per wave for a register/LDS budget of kWaves waves per SIMD: pool +
 // launch parameters must fit 160 KB / (4 kWaves) of LDS, or the CU holds
 // fewer waves than the register budget allows (round 1 lost 7% to an 8-byte
 // LaunchParams growth that pushed the workgroup to 10248 bytes).  Derived from
-// sizeof(LaunchParams): 118 slots at 4 waves per SIMD, 94 at 5, 158 at 3.
-template <int kWaves>
+// sizeof(LaunchParams): 64 LDS bytes per slot, 154 slots at 4 waves per SIMD,
+// 122 at 5.  The pool size matters: lanes step only while the pool holds
+// track-ready paths besides the events waiting for a batch (93 slots instead
+// of 118 at 4 waves cost 13% on C2).
+template <int kWaves, bool kSplit>
 struct PoolSize {
   static constexpr int kBudget = 163840 / (4 * kWaves);  // LDS bytes per one-wave workgroup
   static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
-  static constexpr int value = (kBudget - kParams - 16) / (80 + 4);  // 80-byte slot + 4 list bytes
+#ifdef CVR_WPOOL_SLOTS  // experiment builds: a smaller pool
+  static constexpr int value = CVR_WPOOL_SLOTS;
+#else
+  static constexpr int value = (kBudget - kParams - 16 - 4 * STAT_COUNT) / (kSplit ? 64 : 80);
+#endif
 };
+// Sparse media (C5) keep the event part in LDS too: their cell-leaf pool
+// thrashes L2, so the split's T reads would go to HBM (C5: 156.8 ms split at
+// 4 waves, 153.7 at 5, vs 147 with T in LDS).
+#ifndef CVR_WPOOL_SPLIT_SPARSE
+#define CVR_WPOOL_SPLIT_SPARSE 0
+#endif
 
-// One path per slot, array-of-structs in 16-byte blocks so a path moves with
-// ds_read_b128 / ds_write_b128 (5 per full path instead of 19 dword ops):
+// One path per slot.  LDS holds what the track loop and the event code both
+// need, as arrays of 16-byte blocks (ds_read_b128 / ds_write_b128):
 //   a = (o.x, o.y, o.z, t)   b = (d.x, d.y, d.z, dist)   c = rng v0..v3
-//   e = (rng v4, rng d, image_id, meta)   f = (T.x, T.y, T.z, -)
-// meta: bits 0-2 normal code, bit 3 inside, bits 4.. segments so far.
-struct alignas(16) PoolSlot {
-  float4 a, b;
-  uint4 c, e;
-  float4 f;
-};
-template <int kSlots>
+//   e = (rng v4, rng d)      meta: bits 0-2 normal code, bit 3 inside, bits 4.. segments
+// The event-only part, (T.x, T.y, T.z, image_id), lives in global memory
+// (L.pool_T, one float4 per slot of every wave: ~10 MB, L2-resident), read
+// and written once per event; so a slot takes 64 LDS bytes instead of 84 and
+// the pool holds 30% more paths, enough for 5 waves per SIMD (C2: 5.25 ms
+// vs 5.40 at 4 waves with the whole slot in LDS).  !kSplit: f in LDS.
+template <int kSlots, bool kSplit>
 struct WavePool {
-  PoolSlot p[kSlots];
+  float4 a[kSlots], b[kSlots];
+  uint4 c[kSlots];
+  float4 f[kSplit ? 1 : kSlots];  // (T, image_id) when not split
+  uint2 e[kSlots];
+  uint32_t meta[kSlots];
   uint8_t ready[kSlots];   // ring of track-ready slots
   uint8_t lb[kSlots];      // stack of boundary events
   uint8_t lc[kSlots];      // stack of real collisions
   uint8_t ln[kSlots];      // stack of slots waiting for a new path
+  uint32_t cnt[STAT_COUNT];  // the wave's event counters (lane 0 adds per batch)
 };
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
@@ -92,49 +117,50 @@ __device__ __forceinline__ V3 normal_of(uint32_t c) {
   return c == 0u ? mk3(0, 0, 0) : c <= 2u ? mk3(s, 0, 0) : c <= 4u ? mk3(0, s, 0) : mk3(0, 0, s);
 }
 
-template <int kSlots>
-__device__ __forceinline__ void store_full(WavePool<kSlots>& S, uint32_t s, const PathState& ps, const Isect& is,
-                                           uint32_t nseg) {
-  PoolSlot& q = S.p[s];
-  q.a = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
-  q.b = make_float4(ps.d.x, ps.d.y, ps.d.z, is.dist);
-  q.c = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);
-  q.e = make_uint4(ps.rng.v4, ps.rng.d, ps.image_id, normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4));
-  q.f = make_float4(ps.T.x, ps.T.y, ps.T.z, 0.0f);
+template <int kSlots, bool kSplit>
+__device__ __forceinline__ void store_full(WavePool<kSlots, kSplit>& S, float4* __restrict__ gT, uint32_t s,
+                                           const PathState& ps, const Isect& is, uint32_t nseg) {
+  S.a[s] = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
+  S.b[s] = make_float4(ps.d.x, ps.d.y, ps.d.z, is.dist);
+  S.c[s] = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);
+  S.e[s] = make_uint2(ps.rng.v4, ps.rng.d);
+  S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
+  const float4 f = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
+  if constexpr (kSplit) gT[s] = f;
+  else S.f[s] = f;
 }
-template <int kSlots>
-__device__ __forceinline__ void load_full(const WavePool<kSlots>& S, uint32_t s, PathState& ps, Isect& is, uint32_t& nseg,
-                                          float& t) {
-  const PoolSlot& q = S.p[s];
-  const float4 a = q.a, b = q.b, f = q.f;
-  const uint4 c = q.c, e = q.e;
+template <int kSlots, bool kSplit>
+__device__ __forceinline__ void load_full(const WavePool<kSlots, kSplit>& S, const float4* __restrict__ gT, uint32_t s,
+                                          PathState& ps, Isect& is, uint32_t& nseg, float& t) {
+  const float4 f = kSplit ? gT[s] : S.f[s];
+  const float4 a = S.a[s], b = S.b[s];
+  const uint4 c = S.c[s];
+  const uint2 e = S.e[s];
+  const uint32_t meta = S.meta[s];
   ps.o = mk3(a.x, a.y, a.z);
   t = a.w;
   ps.d = mk3(b.x, b.y, b.z);
   is.dist = b.w;
   ps.T = mk3(f.x, f.y, f.z);
   ps.rng = Rng{c.x, c.y, c.z, c.w, e.x, e.y};
-  ps.image_id = e.z;
-  is.normal = normal_of(e.w & 7u);
-  is.inside = (e.w & 8u) != 0u;
-  nseg = e.w >> 4;
+  ps.image_id = __float_as_uint(f.w);
+  is.normal = normal_of(meta & 7u);
+  is.inside = (meta & 8u) != 0u;
+  nseg = meta >> 4;
 }
-template <int kSlots>
-__device__ __forceinline__ void store_track(WavePool<kSlots>& S, uint32_t s, float t, const Rng& rng) {
-  PoolSlot& q = S.p[s];
-  q.a.w = t;
-  q.c = make_uint4(rng.v0, rng.v1, rng.v2, rng.v3);
-  q.e.x = rng.v4;
-  q.e.y = rng.d;
+template <int kSlots, bool kSplit>
+__device__ __forceinline__ void store_track(WavePool<kSlots, kSplit>& S, uint32_t s, float t, const Rng& rng) {
+  S.a[s].w = t;
+  S.c[s] = make_uint4(rng.v0, rng.v1, rng.v2, rng.v3);
+  S.e[s] = make_uint2(rng.v4, rng.d);
 }
 // Track state of a ready path: o, t, d, max_t, rng.
-template <int kSlots>
-__device__ __forceinline__ void load_track(const WavePool<kSlots>& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
+template <int kSlots, bool kSplit>
+__device__ __forceinline__ void load_track(const WavePool<kSlots, kSplit>& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
                                            float& max_t) {
-  const PoolSlot& q = S.p[s];
-  const float4 a = q.a, b = q.b;
-  const uint4 c = q.c;
-  const uint2 e = make_uint2(q.e.x, q.e.y);
+  const float4 a = S.a[s], b = S.b[s];
+  const uint4 c = S.c[s];
+  const uint2 e = S.e[s];
   o = mk3(a.x, a.y, a.z);
   t = a.w;
   d = mk3(b.x, b.y, b.z);
@@ -154,7 +180,8 @@ struct Cursor {
 
 template <bool kScatterEps, int kWaves, bool kSparse>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
-  constexpr int kSlots = PoolSize<kWaves>::value;
+  constexpr bool kSplit = !kSparse || CVR_WPOOL_SPLIT_SPARSE;
+  constexpr int kSlots = PoolSize<kWaves, kSplit>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
   // branches of the walk code fold away and take no scalar registers.
   MediumParams m = mk;
@@ -164,9 +191,9 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
   }
-  static_assert(sizeof(WavePool<kSlots>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
+  static_assert(sizeof(WavePool<kSlots, kSplit>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves, kSplit>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
-  __shared__ WavePool<kSlots> S;
+  __shared__ WavePool<kSlots, kSplit> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
   // scalars (v_readlane reloads in every Woodcock step).
@@ -174,8 +201,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   const uint32_t lane = threadIdx.x;
   if (lane == 0) L = Lk;
   __syncthreads();
-  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t seg_sum = 0;
+  // Counters.  Event counts are popcounts of ballots that lane 0 adds to the
+  // pool's LDS counters once per batch (no per-lane registers, no SGPRs, live
+  // across the track loop); the track loop counts steps and fetches per lane.
+  uint32_t c_steps = 0, c_fetch = 0;
+  if (lane < (uint32_t)STAT_COUNT) S.cnt[lane] = 0u;
   uint32_t n_over = 0;  // wave-uniform: segments whose last Woodcock step passed max_t
   Cursor cur{0, 0, 0, (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % L.n_queues, false};
   const uint32_t batch = L.batch;  // TRACK: swap finished segments once this many lanes are idle
@@ -273,7 +303,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         // evaluations are steps minus the segments that ended past max_t
         // (counted when filed), so only steps are counted here.
         if (slot >= 0 && fst == 0) {
-          ++c[STAT_STEPS];
+          ++c_steps;
           const float xi = rng_float(rng);
           const float xt = rng_float(rng);
           t = woodcock_advance(m, xi, t);
@@ -282,7 +312,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           } else {
             const WoodcockPoint P = woodcock_point(m, o, d, t);
             if (!(P.qb < xt)) {
-              ++c[STAT_FETCH];
+              ++c_fetch;
               const float rho = m.scale * woodcock_density(m, P);
               if (!(rho * m.inv_sigma < xt)) fst = t < max_t ? 2 : 3;
             }
@@ -303,6 +333,20 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
     // ================================================= EVENT ==============
     __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
+    // Event-code view of the medium: its BSDF / box / albedo fields pass
+    // through opaque_s per batch, so values derived from them (HG and box
+    // constants) are recomputed in the batch instead of being hoisted to the
+    // prologue and held in VGPRs across the track loop (4 waves: 127 -> 119
+    // VGPRs).
+    MediumParams me = m;
+    me.g = opaque_s(m.g);
+    me.ax = opaque_s(m.ax);
+    me.ay = opaque_s(m.ay);
+    me.eta = opaque_s(m.eta);
+    me.inv_eta = opaque_s(m.inv_eta);
+    me.bmin = mk3(opaque_s(m.bmin.x), opaque_s(m.bmin.y), opaque_s(m.bmin.z));
+    me.bmax = mk3(opaque_s(m.bmax.x), opaque_s(m.bmax.y), opaque_s(m.bmax.z));
+    me.albedo_bg = mk3(opaque_s(m.albedo_bg.x), opaque_s(m.albedo_bg.y), opaque_s(m.albedo_bg.z));
     // One batch of up to 64 items, [boundary | collision | new].  New items
     // are regenerated first: a camera path's first segment is an AABB test
     // and, when it hits the box from outside, a boundary event, which then
@@ -371,6 +415,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       uint32_t nseg = 0;
       float t_hit = 0.0f;
       bool to_ready = false, to_lb = false, to_ln = false;
+      bool truncated = false, escaped = false, seg_first = false, seg_next = false;  // counted by ballots
 #if CVR_STAMPS
       unsigned long long t_lap = __builtin_amdgcn_s_memtime();
 #endif
@@ -410,27 +455,27 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             is.normal = mk3(0, 0, 0);
             nseg = 0;
             got = true;
-            ++c[STAT_PATHS];
           }
           cur.next += take;
           given += take;
         }
         // first segment: AABB test (NaiveVolPTsk_kernel.cuh:33-47); a new item
         // that got no path (queues exhausted) leaves its slot empty
+        const uint32_t n_got = (uint32_t)__popcll(__ballot(got));
+        if (lane == 0) S.cnt[STAT_PATHS] += n_got;
         if (got) {
           if (L.max_segments && nseg >= L.max_segments) {
-            ++c[STAT_TRUNCATED];
-            seg_sum += nseg;
+            truncated = true;
             to_ln = true;
           } else {
             ++nseg;
-            if (!aabb_intersect(m, ps.o, ps.d, is)) {
+            seg_first = true;
+            if (!aabb_intersect(me, ps.o, ps.d, is)) {
               splat(L, ps);
-              ++c[STAT_ESCAPED];
-              seg_sum += nseg;
+              escaped = true;
               to_ln = true;
             } else if (is.inside) {
-              store_full(S, s, ps, is, nseg);
+              store_full(S, L.pool_T + (size_t)blockIdx.x * kSlots, s, ps, is, nseg);
               to_ready = true;
             } else {
               kind = K_BOUNDARY;  // enters the box: boundary event in this batch
@@ -441,7 +486,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
       CVR_LAP(9)
 #endif
-      if (lane < tb + tc) load_full(S, s, ps, is, nseg, t_hit);
+      float4* __restrict__ gT = L.pool_T + (size_t)blockIdx.x * kSlots;  // this wave's event-only slot part
+      if (lane < tb + tc) load_full(S, gT, s, ps, is, nseg, t_hit);
       // a filed boundary whose last step passed max_t drew one number too many
       if (lane < tb && !(t_hit <= is.dist)) rng_undo(ps.rng);
 #if CVR_STAMPS
@@ -449,39 +495,35 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
       bool alive = false;
       if (kind == K_BOUNDARY) {
-        boundary_event(m, ps, is);
+        boundary_event(me, ps, is);
         alive = roulette(ps);
       }
 #if CVR_STAMPS
       CVR_LAP(7)
 #endif
       if (kind == K_COLLIDE) {
-        scatter_event<kScatterEps>(m, ps, t_hit);
-        ++c[STAT_ALBEDO];
+        scatter_event<kScatterEps>(me, ps, t_hit);
         alive = roulette(ps);
       }
 #if CVR_STAMPS
       CVR_LAP(8)
 #endif
-      if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {
-        seg_sum += nseg;  // the path died in roulette
-        to_ln = true;
-      }
+      const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
+      if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) to_ln = true;  // the path died in roulette
       // ---- next segment: AABB test of the survivors ----------------------
       if (alive) {
         if (L.max_segments && nseg >= L.max_segments) {
-          ++c[STAT_TRUNCATED];
-          seg_sum += nseg;
+          truncated = true;
           to_ln = true;
         } else {
           ++nseg;
-          if (!aabb_intersect(m, ps.o, ps.d, is)) {
+          seg_next = true;
+          if (!aabb_intersect(me, ps.o, ps.d, is)) {
             splat(L, ps);
-            ++c[STAT_ESCAPED];
-            seg_sum += nseg;
+            escaped = true;
             to_ln = true;
           } else {
-            store_full(S, s, ps, is, nseg);
+            store_full(S, gT, s, ps, is, nseg);
             to_ready = is.inside;  // medium: Woodcock from t = 0
             to_lb = !is.inside;    // no medium: boundary at isect.dist
           }
@@ -490,6 +532,18 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
       t_regen = __builtin_amdgcn_s_memtime();
 #endif
+      // a path's segments are the increments of its nseg (each counted once, as
+      // the reference's per-iteration RAYS_STATISTICS count)
+      {
+        const uint32_t n_seg = (uint32_t)(__popcll(__ballot(seg_first)) + __popcll(__ballot(seg_next)));
+        const uint32_t n_esc = (uint32_t)__popcll(__ballot(escaped)), n_tr = (uint32_t)__popcll(__ballot(truncated));
+        if (lane == 0) {
+          S.cnt[STAT_SEGMENTS] += n_seg;
+          S.cnt[STAT_ALBEDO] += n_alb;
+          S.cnt[STAT_ESCAPED] += n_esc;
+          S.cnt[STAT_TRUNCATED] += n_tr;
+        }
+      }
       const unsigned long long mr = __ballot(to_ready), mb = __ballot(to_lb), mn = __ballot(to_ln);
       if (to_ready) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)s;
       if (to_lb) S.lb[n_lb + lane_rank(mb)] = (uint8_t)s;
@@ -509,15 +563,17 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   }
 
   // ---- counters ------------------------------------------------------------
-  c[STAT_SEGMENTS] = seg_sum;
-  c[STAT_DENSITY] = c[STAT_STEPS];
+  {
+    unsigned long long steps = c_steps, fetch = c_fetch;
 #pragma unroll
-  for (int k = 0; k < STAT_COUNT; ++k) {
-    unsigned long long v = c[k];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if (k == STAT_DENSITY) v -= n_over;  // wave totals: steps minus segments ended past max_t
-    if (lane == 0 && v) atomicAdd(L.stats + k, v);
+    for (int off = 32; off > 0; off >>= 1) {
+      steps += __shfl_xor(steps, off);
+      fetch += __shfl_xor(fetch, off);
+    }
+    // density evaluations: steps minus segments whose last step passed max_t
+    const unsigned long long w[STAT_COUNT] = {S.cnt[STAT_PATHS], S.cnt[STAT_SEGMENTS], steps, steps - n_over,
+                                              S.cnt[STAT_ALBEDO], S.cnt[STAT_ESCAPED], S.cnt[STAT_TRUNCATED], fetch};
+    if (lane < (uint32_t)STAT_COUNT && w[lane]) atomicAdd(L.stats + lane, w[lane]);
   }
 #if CVR_STAMPS
   {
@@ -531,7 +587,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
 template <bool E>
 static const void* wpool_fn(int waves, bool sparse) {
-  if (sparse) return reinterpret_cast<const void*>(&k_wpool<E, 4, true>);
+  if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true>)
+                                 : reinterpret_cast<const void*>(&k_wpool<E, 4, true>);
   if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false>);
   if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false>);
   return reinterpret_cast<const void*>(&k_wpool<E, 4, false>);
@@ -548,8 +605,14 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, 0, s);
 }
 
-hipError_t wpool_occupancy(bool scatter_eps, int waves, int* blocks_per_cu) {
-  const void* fn = scatter_eps ? wpool_fn<true>(waves, false) : wpool_fn<false>(waves, false);
+uint32_t wpool_slots(int waves, bool sparse) {
+  constexpr bool ss = CVR_WPOOL_SPLIT_SPARSE;
+  if (sparse) return waves == 5 ? PoolSize<5, ss>::value : PoolSize<4, ss>::value;
+  return waves == 5 ? PoolSize<5, true>::value : waves == 3 ? PoolSize<3, true>::value : PoolSize<4, true>::value;
+}
+
+hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu) {
+  const void* fn = scatter_eps ? wpool_fn<true>(waves, sparse) : wpool_fn<false>(waves, sparse);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, 0);
 }
 
