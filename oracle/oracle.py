@@ -95,8 +95,9 @@ class Oracle:
     def __init__(self, density, albedo, box_min=(-0.5,) * 3, box_max=(0.5,) * 3, scale=100.0,
                  max_density=None, g=0.0, roughness=(0.1, 0.1), eta=None):
         self.lib = load()
-        self.density = np.ascontiguousarray(density, np.float32)
-        self.albedo = np.ascontiguousarray(albedo, np.float32)
+        # own copies: a Scene's arrays are views of memory the scene frees
+        self.density = np.array(density, np.float32, order="C", copy=True)
+        self.albedo = np.array(albedo, np.float32, order="C", copy=True)
         nz, ny, nx = self.density.shape
         m = OracleMedium()
         m.res[:] = (nx, ny, nz)
@@ -120,9 +121,9 @@ class Oracle:
         nx, ny, nz = (int(v) for v in res)
         o = cls(np.zeros((1, 1, 1), np.float32), np.zeros((1, 1, 1, 4), np.float32), box_min, box_max, scale,
                 max_density, g, roughness, eta)
-        o.table = np.ascontiguousarray(table, np.uint32)
-        o.leaf_density = np.ascontiguousarray(leaf_density, np.float32)
-        o.leaf_albedo = None if leaf_albedo is None else np.ascontiguousarray(leaf_albedo, np.float32)
+        o.table = np.array(table, np.uint32, order="C", copy=True)
+        o.leaf_density = np.array(leaf_density, np.float32, order="C", copy=True)
+        o.leaf_albedo = None if leaf_albedo is None else np.array(leaf_albedo, np.float32, order="C", copy=True)
         m = o.m
         m.res[:] = (nx, ny, nz)
         m.leaves = o.table.ctypes.data_as(C.POINTER(C.c_uint32))
