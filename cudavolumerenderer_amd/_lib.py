@@ -245,6 +245,11 @@ class Scene:
     def max_density(self) -> float:
         return float((self.sparse_medium if self.is_sparse else self.medium).max_density)
 
+    @property
+    def has_albedo(self) -> bool:
+        """Whether the medium stores albedo voxels (a sparse scene may use albedo_bg everywhere)."""
+        return (not self.is_sparse) or bool(self.sparse_medium.leaf_albedo)
+
     def leaves(self):
         """(leaf_table (lz, ly, lx) u32, leaf_density (n, 8, 8, 8), leaf_albedo (n, 8, 8, 8, 4) or
         None, albedo_background) as numpy views owned by the scene."""

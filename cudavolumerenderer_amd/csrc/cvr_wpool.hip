@@ -190,6 +190,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_density = nullptr;
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
+    m.scoarse = nullptr;
   }
   static_assert(sizeof(WavePool<kSlots, kSplit>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves, kSplit>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
@@ -310,8 +311,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           if (!(t <= max_t)) {
             fst = 1;
           } else {
-            const WoodcockPoint P = woodcock_point(m, o, d, t);
-            if (!(P.qb < xt)) {
+            WoodcockPoint P = woodcock_point(m, o, d, t);
+            if (!(P.qb < xt) && woodcock_refine(m, P, xt)) {
               ++c_fetch;
               const float rho = m.scale * woodcock_density(m, P);
               if (!(rho * m.inv_sigma < xt)) fst = t < max_t ? 2 : 3;

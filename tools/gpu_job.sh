@@ -50,6 +50,8 @@ for step in "$@"; do
     prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmcf:*) sc=${step#pmcf:}; mkdir -p "$OUT/pmcf_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcf_$sc/libcvr.sha256"; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcw:*) sc=${step#pmcw:}; mkdir -p "$OUT/pmcw_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcw_$sc/libcvr.sha256"; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    # arbitrary counters on a scene's bench run: pmcx:SCENE:CTR1,CTR2,...
+    pmcx:*) IFS=: read -r _ sc ctrs <<< "$step"; d=pmcx_${sc}_${ctrs//,/_}; mkdir -p "$OUT/$d"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/$d/libcvr.sha256"; run $d 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$OUT/$d" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
     # A/B of experiment builds: ab:SCENE:ROUNDS:variant1,variant2,...
     ab:*) IFS=: read -r _ sc rounds vs <<< "$step"; run ab_$sc 400 bash tools/ab.sh $sc $rounds ${vs//,/ } ;;
     *) echo "unknown step $step" ;;
