@@ -907,7 +907,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       if (v != 3 && v != 4 && v != 5 && v != 6 && v != 8)
         return set_err(&c->err, CVR_ERR_INVALID, "waves must be 3, 4, 5, 6 or 8");
       c->waves = (int)v;
-      c->wpool_waves = (v == 5 || v == 3) ? (int)v : 4;
+      c->wpool_waves = (v == 5 || v == 3 || v == 6) ? (int)v : 4;
       c->inited = false;
       return CVR_OK;
     case CVR_OPT_BATCH:

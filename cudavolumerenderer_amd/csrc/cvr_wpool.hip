@@ -591,6 +591,7 @@ static const void* wpool_fn(int waves, bool sparse) {
   if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true>)
                                  : reinterpret_cast<const void*>(&k_wpool<E, 4, true>);
   if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false>);
+  if (waves == 6) return reinterpret_cast<const void*>(&k_wpool<E, 6, false>);
   if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false>);
   return reinterpret_cast<const void*>(&k_wpool<E, 4, false>);
 }
@@ -609,7 +610,10 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
 uint32_t wpool_slots(int waves, bool sparse) {
   constexpr bool ss = CVR_WPOOL_SPLIT_SPARSE;
   if (sparse) return waves == 5 ? PoolSize<5, ss>::value : PoolSize<4, ss>::value;
-  return waves == 5 ? PoolSize<5, true>::value : waves == 3 ? PoolSize<3, true>::value : PoolSize<4, true>::value;
+  return waves == 5   ? PoolSize<5, true>::value
+         : waves == 6 ? PoolSize<6, true>::value
+         : waves == 3 ? PoolSize<3, true>::value
+                      : PoolSize<4, true>::value;
 }
 
 hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu) {
