@@ -109,6 +109,9 @@ def load() -> C.CDLL:
         "cvr_set_iterations": (I32, [P, U32]),
         "cvr_set_path_range": (I32, [P, U64, U64]),
         "cvr_set_block_shard": (I32, [P, U32, U32]),
+        "cvr_set_block_order": (I32, [P, P, U32]),
+        "cvr_share_medium": (I32, [P, P]),
+        "cvr_launch_blocks": (I32, [P, P, P, P]),
         "cvr_set_seed": (I32, [P, U32]),
         "cvr_get_seed": (I32, [P, C.POINTER(U32)]),
         "cvr_set_output": (I32, [P, P]),
@@ -356,6 +359,26 @@ class Context:
     def set_block_shard(self, rank, world):
         """Launch only shard `rank` of `world` (cvr_set_block_shard)."""
         self._c(load().cvr_set_block_shard(self._h, rank, world))
+
+    def share_medium(self, src: "Context"):
+        """Render `src`'s medium without a copy (cvr_share_medium); keep `src` alive."""
+        self._c(load().cvr_share_medium(self._h, src._h))
+        self._medium_src = src
+
+    def set_block_order(self, perm: Optional[np.ndarray]):
+        """Block work order of the launch (cvr_set_block_order); None = natural."""
+        if perm is None:
+            self._c(load().cvr_set_block_order(self._h, None, 0))
+            return
+        p = np.ascontiguousarray(perm, np.uint32)
+        self._c(load().cvr_set_block_order(self._h, p.ctypes.data_as(C.c_void_p), len(p)))
+
+    def launch_blocks(self):
+        """(n_blocks, n_queues, qbeg) of the current launch's pixel-block work order."""
+        nb, nq = C.c_uint32(), C.c_uint32()
+        qb = (C.c_uint32 * 9)()
+        self._c(load().cvr_launch_blocks(self._h, C.byref(nb), C.byref(nq), qb))
+        return nb.value, nq.value, list(qb)[:nq.value + 1]
 
     def set_seed(self, seed):
         self._c(load().cvr_set_seed(self._h, seed))

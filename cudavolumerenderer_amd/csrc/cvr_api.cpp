@@ -81,6 +81,8 @@ struct cvr_ctx {
   float4* d_leaf_albedo = nullptr;
   uint32_t* d_sbounds = nullptr;
   uint32_t* d_scoarse = nullptr;
+  uint32_t* d_block_perm = nullptr;  // cvr_set_block_order
+  uint32_t block_perm_n = 0;
   size_t n_cell_leaves = 0;  // cell-leaf pool slots (incl. the zero slot)
   bool have_medium = false;
   cvr::MediumParams m{};
@@ -111,7 +113,7 @@ struct cvr_ctx {
 
   // options
   uint32_t max_segments = 1u << 20;
-  uint32_t chunk = 256;
+  uint32_t chunk = 0;  // paths per wave dequeue; 0: auto (wave pool: 64..256 by the launch's size, others 256)
   uint32_t ev_thresh = 56;
   uint32_t grid_override = 0;
   int scatter_eps = -1;
@@ -201,6 +203,7 @@ int ensure_output(cvr_ctx* c) {
   if (px == 0) return set_err(&c->err, CVR_ERR_STATE, "resolution not set");
   if (c->out_owned_px < px) {
     if (c->d_out_owned) (void)hipFree(c->d_out_owned);
+  if (c->d_block_perm) (void)hipFree(c->d_block_perm);
     c->d_out_owned = nullptr;
     HIP_TRY(c, hipMalloc(&c->d_out_owned, px * sizeof(float4)));
     HIP_TRY(c, hipMemsetAsync(c->d_out_owned, 0, px * sizeof(float4), c->stream));
@@ -287,6 +290,7 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   }
   for (uint32_t q = 0; q <= 8; ++q)
     L.qbeg[q] = q <= L.n_queues ? (uint32_t)((uint64_t)L.n_blocks * q / L.n_queues) : L.n_blocks;
+  L.block_perm = (L.order == 1 && c->d_block_perm && c->block_perm_n == L.n_blocks) ? c->d_block_perm : nullptr;
   L.div_tile_px = make_fastdiv(L.tile_px);
   L.div_tile_w = make_fastdiv(L.tile_w);
   L.div_block = make_fastdiv(64u * L.samples);
@@ -772,6 +776,33 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
   return CVR_OK;
 }
 
+int cvr_share_medium(cvr_ctx* c, const cvr_ctx* src) {
+  if (!c || !src) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (c == src) return CVR_OK;
+  if (!src->have_medium) return set_err(&c->err, CVR_ERR_STATE, "source context has no medium");
+  if (src->device != c->device)
+    return set_err(&c->err, CVR_ERR_INVALID, "source context is on device %d, not %d", src->device, c->device);
+  int r = ensure_device(c);
+  if (r) return r;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  // drop this context's own medium; the kernels read the source's buffers
+  if (c->d_density) (void)hipFree(c->d_density);
+  if (c->d_albedo) (void)hipFree(c->d_albedo);
+  if (c->d_cells) (void)hipFree(c->d_cells);
+  if (c->d_bounds) (void)hipFree(c->d_bounds);
+  c->d_density = nullptr;
+  c->d_albedo = nullptr;
+  c->d_cells = nullptr;
+  c->d_bounds = nullptr;
+  c->n_voxels = 0;
+  free_sparse(c);
+  c->m = src->m;
+  c->n_cell_leaves = src->n_cell_leaves;
+  c->have_medium = true;
+  c->inited = false;
+  return CVR_OK;
+}
+
 int cvr_set_camera(cvr_ctx* c, const float inv_view[12], const float r2v[2], const float full_res[2]) {
   if (!c || !inv_view || !r2v || !full_res) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   memcpy(c->inv_view, inv_view, sizeof(c->inv_view));
@@ -827,6 +858,38 @@ int cvr_set_block_shard(cvr_ctx* c, uint32_t rank, uint32_t world) {
   if (world == 0 || rank >= world) return set_err(&c->err, CVR_ERR_INVALID, "bad shard %u of %u", rank, world);
   c->shard_rank = rank;
   c->shard_world = world;
+  return CVR_OK;
+}
+
+int cvr_set_block_order(cvr_ctx* c, const uint32_t* perm, uint32_t n) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  if (c->d_block_perm) (void)hipFree(c->d_block_perm);
+  c->d_block_perm = nullptr;
+  c->block_perm_n = 0;
+  if (!perm || n == 0) return CVR_OK;  // natural order
+  std::vector<uint8_t> seen(n, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (perm[i] >= n || seen[perm[i]])
+      return set_err(&c->err, CVR_ERR_INVALID, "block order is not a permutation of [0, %u)", n);
+    seen[perm[i]] = 1;
+  }
+  int r = ensure_device(c);
+  if (r) return r;
+  HIP_TRY(c, hipMalloc(&c->d_block_perm, (size_t)n * sizeof(uint32_t)));
+  HIP_TRY(c, hipMemcpy(c->d_block_perm, perm, (size_t)n * sizeof(uint32_t), hipMemcpyHostToDevice));
+  c->block_perm_n = n;
+  return CVR_OK;
+}
+
+int cvr_launch_blocks(const cvr_ctx* c, uint32_t* n_blocks, uint32_t* n_queues, uint32_t qbeg[9]) {
+  if (!c || !n_blocks || !n_queues || !qbeg) return set_err(nullptr, CVR_ERR_INVALID, "NULL argument");
+  cvr::LaunchParams L{};
+  uint64_t first = 0, count = 0;
+  compute_range(c, &first, &count);
+  fill_launch(c, L, first, count);
+  *n_blocks = L.order == 1 ? L.n_blocks : 0;
+  *n_queues = L.n_queues;
+  for (int q = 0; q < 9; ++q) qbeg[q] = L.qbeg[q];
   return CVR_OK;
 }
 
@@ -967,6 +1030,15 @@ int cvr_launch_render(cvr_ctx* c) {
   cvr::LaunchParams L{};
   fill_launch(c, L, first, count);
   const bool eps = scatter_eps_for(c);
+  if (!c->chunk && scheduler_for(c) == 3 && !c->grid_override) {
+    // Wave-pool dequeue chunk by the paths each wave gets: about 8 chunks per
+    // wave, 64..256 paths.  Small launches (block shards of a multi-GPU render)
+    // then end with the waves' last chunks evenly spread (C2 shard 1/8 on one
+    // GPU: 1.09 ms at 64 vs 1.18 at 256; the whole C2 launch keeps 256).
+    const uint64_t grid = (uint64_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
+    const uint64_t per_wave = grid ? (uint64_t)L.path_count / grid : 0;
+    L.chunk = per_wave >= 2048 ? 256u : per_wave >= 1024 ? 128u : 64u;
+  }
   // The persistent schedulers' u32 queue heads run past a queue's end by at
   // most one chunk per wave before every wave sees the queue exhausted
   // (waves: at most 4 per block of any scheduler).

@@ -199,6 +199,10 @@ struct LaunchParams {
   // blocks blk_off, blk_off + blk_stride, ...; local block b is tile block
   // blk_off + b * blk_stride (0 / 1: the whole tile).
   uint32_t blk_off, blk_stride;
+  // Block order (cvr_set_block_order; null = natural): the b-th block of the
+  // launch is block_perm[b] (a permutation of [0, n_blocks)), e.g. costly
+  // blocks first so that the launch does not end on their long paths.
+  const uint32_t* block_perm;
   uint32_t qbeg[9];       // first block of each queue's band (order 1), qbeg[n_queues] = n_blocks
   FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x;  // by tile_px, tile_w, 64*samples, blocks_x
 };
@@ -215,7 +219,9 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.order == 0) return L.path_first + u;
   const uint32_t per_block = 64u * L.samples;
   const uint32_t bq = fastdiv(u, L.div_block);
-  const uint32_t b = L.blk_off + __umul24(queue_blocks_begin(L, q) + bq, L.blk_stride);
+  uint32_t bl = queue_blocks_begin(L, q) + bq;
+  if (L.block_perm) bl = L.block_perm[bl];
+  const uint32_t b = L.blk_off + __umul24(bl, L.blk_stride);
   const uint32_t rem = u - bq * per_block;
   const uint32_t s = rem >> 6, lane = rem & 63u;
   const uint32_t by = fastdiv(b, L.div_blocks_x);

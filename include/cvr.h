@@ -61,7 +61,8 @@ typedef enum {
 /* Options for cvr_set_option. */
 typedef enum {
   CVR_OPT_MAX_SEGMENTS = 1,   /* safety cap on segments per path (default 1<<20, 0 = none) */
-  CVR_OPT_CHUNK = 2,          /* paths per wave dequeue (persistent schedulers) */
+  CVR_OPT_CHUNK = 2,          /* paths per wave dequeue (persistent schedulers); 0 (default): 256, the
+                                 wave pool 64..256 by the paths each of its waves gets */
   CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
   CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
   CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
@@ -169,6 +170,11 @@ int cvr_set_medium(cvr_ctx* ctx, const cvr_medium_desc* medium);
  * brick bounds are built on the device for the leaves whose cells can
  * interpolate a non-zero density (a brick-pool instead of dense cells). */
 int cvr_set_medium_sparse(cvr_ctx* ctx, const cvr_sparse_medium_desc* medium);
+/* Extension: `ctx` renders the medium of `src` (same device) without a copy:
+ * its kernels read src's device buffers, which stay owned by src (destroy
+ * `ctx` first, or give it a medium of its own, before `src` changes or frees
+ * its medium).  For several contexts with renders in flight on one GPU. */
+int cvr_share_medium(cvr_ctx* ctx, const cvr_ctx* src);
 /* copyInvViewMatrix (12 floats), copyRasterToView, copyPixelIndexRange */
 int cvr_set_camera(cvr_ctx* ctx, const float inv_view[12], const float raster_to_view[2],
                    const float full_res[2]);
@@ -191,6 +197,17 @@ int cvr_set_path_range(cvr_ctx* ctx, uint64_t first, uint64_t count);
  * to the path id, so their summed images equal the unsharded render up to
  * fp32 summation order.  (0, 1) = no shard (default). */
 int cvr_set_block_shard(cvr_ctx* ctx, uint32_t rank, uint32_t world);
+/* Extension (scheduling only; results are bound to path ids): the order in
+ * which the pixel-block work order hands out its blocks.  `perm` is a
+ * permutation of [0, n) with n = the launch's block count (cvr_launch_blocks);
+ * block b of the launch is taken as perm[b]'s turn.  Applies to launches with
+ * that block count; NULL / n = 0 restores the natural order.  Used to start
+ * costly blocks first (cvr_plan_block_order), so a launch does not end on
+ * their long paths running on few lanes. */
+int cvr_set_block_order(cvr_ctx* ctx, const uint32_t* perm, uint32_t n);
+/* The pixel-block work order of the current launch configuration: its block
+ * count (0 = not block ordered), its queues and their bands qbeg[0..n_queues]. */
+int cvr_launch_blocks(const cvr_ctx* ctx, uint32_t* n_blocks, uint32_t* n_queues, uint32_t qbeg[9]);
 /* RNG seed base (RegenerationVolPTsk_kernel.cuh:18 `seed`); path p uses
  * curand_init(seed + p). */
 int cvr_set_seed(cvr_ctx* ctx, uint32_t seed);

@@ -1,0 +1,153 @@
+"""Several renders in flight on one GPU (bench.py's pipelined mode): contexts
+that share one device medium (cvr_share_medium), the pixel-block work order's
+permutation (cvr_set_block_order) and the wave pool's automatic dequeue chunk
+for small launches (block shards).  All are scheduling only: the RNG is bound
+to the path id, so counters are equal and pixels agree up to fp32 summation
+order (tests/parity_util.py), here against the CPU oracle and against the
+plain single-context render."""
+import numpy as np
+import pytest
+
+from parity_util import assert_counters_equal, assert_pixels_close, oracle_for_scene
+
+pytestmark = pytest.mark.gpu
+
+W = H = 256
+ITERS = 6
+
+
+def _owner(cvr, scene):
+    c = cvr.Context(0, "regenerationSK")
+    if scene.is_sparse:
+        c.set_medium_sparse(scene.sparse_medium)
+    else:
+        c.set_medium(scene.medium)
+    return c
+
+
+def _setup(cvr, c):
+    iv, r2v = cvr.default_camera(W, H)
+    c.set_camera(iv, r2v, (W, H))
+    c.init()
+    c.set_resolution(W, H)
+    c.set_iterations(ITERS)
+    return iv, r2v
+
+
+def _render(c):
+    c.clear_output()
+    c.launch_render()
+    st = c.stats()
+    return c.copy_output(W, H), st
+
+
+@pytest.mark.parametrize("name", ["manix", "hetvol"])
+def test_shared_medium_contexts_render_like_the_owner_and_the_oracle(cvr, oracle_mod, name):
+    scene = cvr.Scene.synthetic(name)
+    a = _owner(cvr, scene)
+    iv, r2v = _setup(cvr, a)
+    b = cvr.Context(0, "regenerationSK")
+    b.share_medium(a)
+    _setup(cvr, b)
+    b.use_own_stream()
+    ia, sa = _render(a)
+    ib, sb = _render(b)
+    for k in ("paths", "segments", "steps", "density", "albedo", "escaped", "fetches"):
+        assert getattr(sa, k) == getattr(sb, k), k
+    assert_pixels_close(ib, ia, ITERS, "shared medium")
+    orc = oracle_for_scene(oracle_mod, scene)
+    ref, rst = orc.render(orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 2, 0), 0, W * H * ITERS, nthreads=8)
+    assert_counters_equal(sb, rst, "shared medium vs oracle")
+    assert_pixels_close(ib, ref, ITERS, "shared medium vs oracle")
+    b.close()
+    a.close()
+
+
+def test_renders_in_flight_on_two_streams_match(cvr):
+    """Launch on three contexts (own streams) back to back without syncs, as
+    bench.py's pipelined step does; every image equals the serial one."""
+    scene = cvr.Scene.synthetic("manix")
+    a = _owner(cvr, scene)
+    _setup(cvr, a)
+    ref, rs = _render(a)
+    ctxs = [a]
+    for _ in range(2):
+        c = cvr.Context(0, "regenerationSK")
+        c.share_medium(a)
+        _setup(cvr, c)
+        c.use_own_stream()
+        ctxs.append(c)
+    a.use_own_stream()
+    for c in ctxs:
+        c.clear_output()
+        c.launch_render()
+    for c in ctxs:
+        c.synchronize()
+        img, st = c.copy_output(W, H), c.stats()
+        assert st.steps == rs.steps and st.escaped == rs.escaped
+        assert_pixels_close(img, ref, ITERS, "in flight")
+    for c in reversed(ctxs):
+        c.close()
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_block_order_permutation_changes_nothing(cvr, oracle_mod, world):
+    scene = cvr.Scene.synthetic("manix")
+    c = _owner(cvr, scene)
+    iv, r2v = _setup(cvr, c)
+    c.set_path_range(0, W * H * ITERS)
+    c.set_block_shard(world - 1, world)
+    nat, sn = _render(c)
+    nb, nq, qbeg = c.launch_blocks()
+    assert nb == len(range(world - 1, (W // 8) * (H // 8), world)) and qbeg[-1] == nb
+    perm = np.random.default_rng(7).permutation(nb).astype(np.uint32)
+    c.set_block_order(perm)
+    per, sp = _render(c)
+    for k in ("paths", "segments", "steps", "density", "albedo", "escaped", "fetches"):
+        assert getattr(sn, k) == getattr(sp, k), k
+    assert_pixels_close(per, nat, ITERS, "block order")
+    with pytest.raises(cvr.CvrError):
+        c.set_block_order(np.zeros(nb, np.uint32))  # not a permutation
+    c.set_block_order(None)
+    again, _ = _render(c)
+    assert_pixels_close(again, nat, ITERS, "natural again")
+    c.close()
+
+
+def test_small_shard_auto_chunk_vs_oracle(cvr, oracle_mod):
+    """A C2-sized block shard 7 of 8 (the per-rank launch of an 8-GPU
+    strong-scaling render, where the wave pool's dequeue chunk drops to 64): pixels and
+    counters vs the oracle's render of the same path ids."""
+    from cudavolumerenderer_amd.distributed import block_shard_path_ids
+    scene = cvr.Scene.synthetic("manix")
+    Wc = Hc = 1024
+    iters = 4  # 131 K paths per shard: about 26 per wave, chunk 64
+    c = cvr.Context(0, "regenerationSK")
+    c.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(Wc, Hc)
+    c.set_camera(iv, r2v, (Wc, Hc))
+    c.init()
+    c.set_resolution(Wc, Hc)
+    c.set_iterations(iters)
+    c.set_path_range(0, Wc * Hc * iters)
+    c.set_block_shard(7, 8)
+    c.clear_output()
+    c.launch_render()
+    st = c.stats()
+    img = c.copy_output(Wc, Hc)
+    ids = block_shard_path_ids(Wc, Hc, iters, 7, 8)
+    orc = oracle_for_scene(oracle_mod, scene)
+    L = orc.launch(iv, r2v, (Wc, Hc), (Wc, Hc), (0, 0), 2, 0)
+    # the shard's path ids are runs of 8 consecutive ids (one block row of one sample)
+    ref = np.zeros((Hc, Wc, 4), np.float32)
+    steps = esc = 0
+    for start in ids[::8]:
+        rec = orc.trace_paths(L, int(start), 8)
+        steps += int(rec["n_steps"].sum())
+        e = rec[(rec["flags"] & 1) != 0]
+        np.add.at(ref.reshape(-1, 4)[:, :3], e["image_id"], e["T"])
+        ref.reshape(-1, 4)[e["image_id"], 3] = 1.0
+        esc += len(e)
+    assert st.paths == len(ids) and st.steps == steps and st.escaped == esc
+    assert_pixels_close(img, ref, iters, "shard 7/8")
+    c.close()

@@ -94,6 +94,9 @@ def main():
         c.init()
         c.set_resolution(W, H)
         c.set_iterations(a.iters)
+        if "shard" in d:  # block shard `rank` of `shard` (bench.py's strong-scaling split), one GPU
+            c.set_path_range(0, W * H * a.iters)
+            c.set_block_shard(d.get("rank", 0), d["shard"])
         ctxs.append((v, c))
     times = {v: [] for v, _ in ctxs}
     extra = {}
