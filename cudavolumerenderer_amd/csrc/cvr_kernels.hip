@@ -102,7 +102,7 @@ template <bool kScatterEps>
 __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, PathRecord* rec) {
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= L.path_count) return;
-  if (L.naive_mk) {
+  if (L.naive_mk & 1u) {
     const MkResult mr = walk_mk(m, L, L.path_first + tid);
     PathRecord r = {};
     r.image_id = (L.path_first + tid) % L.tile_px;

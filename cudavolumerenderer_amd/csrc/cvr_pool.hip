@@ -55,7 +55,62 @@ struct PoolLds {
   uint16_t lc[kSlots];        // real collisions (appended by TRACK, read by EVENT)
   uint32_t n_ready[2], n_lb[2], n_lc, n_new, ready_head;
   uint32_t cur_next, cur_end, cur_q, exhausted;  // workgroup path cursor into the global queues
+  uint32_t skey[512];  // Morton sort of a track phase's ready list (streamingSK): code << 9 | slot
 };
+static_assert(kSlots <= 512, "Morton sort keys hold 9-bit slot indices");
+
+// Utilities.h:35-55: 30-bit Morton code of a point in the unit cube.
+__device__ __forceinline__ uint32_t expand_bits(uint32_t v) {
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+__device__ __forceinline__ uint32_t morton3d(float x, float y, float z) {
+  x = fminf(fmaxf(x * 1024.0f, 0.0f), 1023.0f);
+  y = fminf(fmaxf(y * 1024.0f, 0.0f), 1023.0f);
+  z = fminf(fmaxf(z * 1024.0f, 0.0f), 1023.0f);
+  return expand_bits((uint32_t)x) * 4u + expand_bits((uint32_t)y) * 2u + expand_bits((uint32_t)z);
+}
+
+// streamingSK's ray order (StreamingVolPTsk_kernel.cuh:188-216,
+// MortonSort.h:28-49): the track phase's ready paths sorted by the Morton code
+// of their origin in the box (AABB::transform), so the lanes of a wave, which
+// take consecutive ready entries, trace nearby rays.  Bitonic sort of up to
+// 512 keys (the code's top 23 bits above the 9-bit slot) by the workgroup.
+// Scheduling only: every path still runs its own RNG stream.
+__device__ void morton_sort_ready(PoolLds& S, const MediumParams& m, uint16_t* ready, uint32_t n) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t P = 64u;
+  while (P < n) P <<= 1;
+  const V3 ext = sub3(m.bmax, m.bmin);
+  for (uint32_t i = tid; i < P; i += kThreads) {
+    uint32_t key = 0xFFFFFFFFu;
+    if (i < n) {
+      const uint32_t sl = ready[i];
+      const V3 p = div3(sub3(mk3(S.ox[sl], S.oy[sl], S.oz[sl]), m.bmin), ext);
+      key = ((morton3d(p.x, p.y, p.z) >> 7) << 9) | sl;
+    }
+    S.skey[i] = key;
+  }
+  __syncthreads();
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t t = tid; t < P / 2; t += kThreads) {
+        const uint32_t lo = ((t & ~(j - 1u)) << 1) | (t & (j - 1u)), hi = lo + j;
+        const uint32_t a = S.skey[lo], b = S.skey[hi];
+        if ((a > b) == ((lo & k) == 0u)) {
+          S.skey[lo] = b;
+          S.skey[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = tid; i < n; i += kThreads) ready[i] = (uint16_t)(S.skey[i] & 511u);
+  __syncthreads();
+}
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -330,6 +385,7 @@ __global__ __launch_bounds__(kThreads, 4) void k_pool(MediumParams m, LaunchPara
     __syncthreads();
     CVR_STAMP(1)
     if (done) break;
+    if ((L.naive_mk & 2u) && S.n_ready[rp] > 64u) morton_sort_ready(S, m, S.ready[rp], S.n_ready[rp]);
 
     // ========================================================== TRACK ======
     {

@@ -183,7 +183,8 @@ struct LaunchParams {
   uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
   uint32_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track
   uint32_t batch;         // wave-pool kernel: idle lanes that trigger a swap
-  uint32_t naive_mk;      // trace kernel: naiveMK paths (walk_mk) instead of path_begin + loop
+  uint32_t naive_mk;      // bit 0: trace kernel runs naiveMK paths (walk_mk) instead of path_begin + loop;
+                          // bit 1: pool kernel sorts each track phase's paths by Morton code (streamingSK)
   // Work order (scheduling only; results are bound to path ids).  order 0:
   // path ids in sample-major order from one queue.  order 1: 8x8-pixel
   // blocks with all their samples back to back (path_first must be a

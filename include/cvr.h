@@ -82,13 +82,17 @@ typedef enum {
                                  identical either way. */
   CVR_OPT_TAIL = 14,          /* pool scheduler: lanes below which a wave ends a track phase (16) */
   CVR_OPT_BATCH = 15,         /* wave-pool scheduler: idle lanes that trigger a refill (8) */
-  CVR_OPT_RNG_BINDING = 16    /* regenerationSK: 0 (default) RNG bound to the path id (Q2 fixed:
+  CVR_OPT_RNG_BINDING = 16,   /* regenerationSK: 0 (default) RNG bound to the path id (Q2 fixed:
                                  deterministic, scheduler-independent); 1 the reference's binding,
                                  Rng(seed + tid) per persistent thread, roulette draw after an
                                  escape, isect kept across a thread's paths
                                  (RegenerationVolPTsk_kernel.cuh:146-232).  Thread-bound results
                                  depend on which thread takes which path: deterministic only for a
                                  one-wave launch (CVR_OPT_GRID 1). */
+  CVR_OPT_MORTON = 17          /* pool scheduler (streamingSK): 1 sorts each track phase's paths by the
+                                 Morton code of their origin in the box (MortonSort.h:28-49,
+                                 StreamingVolPTsk_kernel.cuh:188-216); default 0 (measured slower
+                                 here).  Scheduling only: results are unchanged. */
 } cvr_option;
 
 /* HeterogeneousMedium + GGX boundary (Medium.h:110-190, Bsdf.h:17-30). */

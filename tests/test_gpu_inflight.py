@@ -151,3 +151,28 @@ def test_small_shard_auto_chunk_vs_oracle(cvr, oracle_mod):
     assert st.paths == len(ids) and st.steps == steps and st.escaped == esc
     assert_pixels_close(img, ref, iters, "shard 7/8")
     c.close()
+
+
+@pytest.mark.parametrize("name", ["manix", "hetvol"])
+def test_morton_sorted_track_order_vs_oracle(cvr, oracle_mod, name):
+    """streamingSK with the reference's Morton ray order (CVR_OPT_MORTON 1,
+    StreamingVolPTsk_kernel.cuh:188-216) on the pool scheduler: counters equal
+    and pixels within the summation bound against the oracle's streamingSK
+    render (scatter -eps, kernel id 4) and the unsorted run."""
+    scene = cvr.Scene.synthetic(name)
+    imgs = []
+    for morton in (0, 1):
+        c = cvr.Context(0, "streamingSK")
+        c.set_option(cvr.OPT_MORTON, morton)
+        c.set_medium(scene.medium)
+        iv, r2v = _setup(cvr, c)
+        imgs.append(_render(c))
+        c.close()
+    (i0, s0), (i1, s1) = imgs
+    for k in ("paths", "segments", "steps", "density", "albedo", "escaped", "fetches"):
+        assert getattr(s0, k) == getattr(s1, k), k
+    orc = oracle_for_scene(oracle_mod, scene)
+    ref, rst = orc.render(orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 4, 0), 0, W * H * ITERS, nthreads=8)
+    assert_counters_equal(s1, rst, "morton vs oracle")
+    assert_pixels_close(i1, ref, ITERS, "morton vs oracle")
+    assert_pixels_close(i1, i0, ITERS, "morton vs unsorted")

@@ -1,0 +1,39 @@
+#!/bin/bash
+# One measurement pass of the committed build on the GPU box (gpurun):
+# GPU tests, bench lines for C1-C5, rocprofv3 kernel stats (C2, C3, C5), PMC
+# traffic passes (FETCH_SIZE / WRITE_SIZE, separate runs) and the SQ counter
+# groups for C2.  Every step under its own time limit; stops at the first
+# failure.  Output: gpurun_out/final/.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/final
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/libcvr.sha256"
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  local t0=$(date +%s)
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc $(( $(date +%s) - t0 ))s"
+  [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
+}
+B="python3 bench.py --no-cpu-baseline"
+step pytest_gpu 600 python3 -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider
+step c2_bench 200 python3 bench.py --steps 20 --warmup 5
+step c1_bench 200 python3 bench.py --scene bucky --steps 20 --warmup 5
+step c3_bench 200 python3 bench.py --scene hetvol --steps 20 --warmup 5
+step c5_bench 400 python3 bench.py --scene cloud --steps 5 --warmup 1
+step c4_bench 400 $B --shard tiles --resolution 2048 2048 --iterations 256 --steps 2 --warmup 1
+for sc in manix hetvol cloud; do
+  if [ $sc = cloud ]; then S="--steps 3 --warmup 1"; else S="--steps 10 --warmup 2"; fi
+  step prof_$sc 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- $B --scene $sc $S
+  if [ $sc = cloud ]; then S="--steps 2 --warmup 1"; else S="--steps 3 --warmup 1"; fi
+  step pmcf_$sc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
+  step pmcw_$sc 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
+  cp "$OUT/libcvr.sha256" "$OUT/pmcf_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcw_$sc/"
+done
+step pmc_a 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc_a" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
+step pmc_b 200 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc_b" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
+step pmc_c 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc_c" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
+echo "final profile done"

@@ -88,6 +88,8 @@ def main():
             c.set_option(cvr.OPT_BATCH, d["batch"])
         if "tail" in d:
             c.set_option(cvr.OPT_TAIL, d["tail"])
+        if "morton" in d:
+            c.set_option(cvr.OPT_MORTON, d["morton"])
         if "pool" in d:
             c.set_option(cvr.OPT_POOL, d["pool"])
         c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
