@@ -111,6 +111,7 @@ def load() -> C.CDLL:
         "cvr_set_block_shard": (I32, [P, U32, U32]),
         "cvr_set_block_order": (I32, [P, P, U32]),
         "cvr_share_medium": (I32, [P, P]),
+        "cvr_image_to_host": (I32, [P, P, C.c_size_t, C.c_float, P]),
         "cvr_launch_blocks": (I32, [P, P, P, P]),
         "cvr_set_seed": (I32, [P, U32]),
         "cvr_get_seed": (I32, [P, C.POINTER(U32)]),
@@ -184,6 +185,13 @@ def tile_origin(tile_id: int, ntx: int, tile_dim: Sequence[int]):
     org = (C.c_uint32 * 2)()
     _check(lib.cvr_tile_origin(tile_id, ntx, td, org))
     return int(org[0]), int(org[1])
+
+
+def image_to_host(device_ptr: int, host_ptr: int, n_floats: int, scale: float, stream_ptr: Optional[int]):
+    """host[i] = device[i] / scale, written by a kernel on `stream_ptr` into
+    pinned or registered host memory (cvr_image_to_host; asynchronous)."""
+    _check(load().cvr_image_to_host(C.c_void_p(device_ptr), C.c_void_p(host_ptr), n_floats, scale,
+                                    C.c_void_p(stream_ptr) if stream_ptr else None))
 
 
 def write_hdr(path: str, rgba: np.ndarray):

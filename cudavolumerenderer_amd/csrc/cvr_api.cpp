@@ -1141,6 +1141,18 @@ int cvr_clear_output(cvr_ctx* c) {
   return CVR_OK;
 }
 
+int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats, float scale, void* stream) {
+  if (!device_src || !host_dst) return set_err(nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (n_floats == 0) return CVR_OK;
+  void* dptr = nullptr;  // the host buffer's device address (pinned / registered memory)
+  hipError_t e = hipHostGetDevicePointer(&dptr, host_dst, 0);
+  if (e != hipSuccess || !dptr)
+    return set_err(nullptr, CVR_ERR_INVALID, "host buffer is not pinned or registered: %s", hipGetErrorString(e));
+  e = cvr::launch_image_to_host(device_src, static_cast<float*>(dptr), n_floats, scale, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, CVR_ERR_HIP, "image to host: %s", hipGetErrorString(e));
+  return CVR_OK;
+}
+
 int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   if (!c || !st) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -57,6 +57,7 @@ uint32_t wpool_slots(int waves, bool sparse);
 hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
                                hipStream_t s);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
+hipError_t launch_image_to_host(const float* src, float* dst, size_t n, float scale, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);
 // Sparse medium: cell-leaf pool (`coords`: 3 u32 leaf coordinates per slot,

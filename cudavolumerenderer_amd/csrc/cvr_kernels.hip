@@ -8,6 +8,8 @@
 // The production regenerationSK scheduler is cvr_persistent.hip.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "cvr_kernels.h"
 #include "cvr_walk.h"
 
@@ -259,6 +261,43 @@ __global__ __launch_bounds__(256) void k_tile_to_image(const float4* __restrict_
   const uint32_t x = i % tw, y = i / tw;
   const float4 v = tile[i];
   image[(size_t)(y + oy) * iw + (x + ox)] = make_float4(v.x / scale, v.y / scale, v.z / scale, v.w / scale);
+}
+
+// Normalise + store into pinned host memory in one kernel (the transfer
+// delegate's Scale functor and its D->H copy, ImageBufferTransfer.cu:61-78,
+// UtilityFunctors::Scale x/scale, Utilities.h:6-15): the GPU writes the host
+// buffer directly, so the copy is an ordinary kernel in stream order (no copy
+// engine, which here blocked the host on cross-stream dependencies).
+__global__ __launch_bounds__(256) void k_image_to_host(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                       size_t n4, float scale) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    const float4 v = src[i];
+    __builtin_nontemporal_store(v.x / scale, &dst[i].x);
+    __builtin_nontemporal_store(v.y / scale, &dst[i].y);
+    __builtin_nontemporal_store(v.z / scale, &dst[i].z);
+    __builtin_nontemporal_store(v.w / scale, &dst[i].w);
+  }
+}
+// unaligned buffers and the ragged tail, one float per work-item
+__global__ __launch_bounds__(256) void k_image_to_host_scalar(const float* __restrict__ src, float* __restrict__ dst,
+                                                             size_t first, size_t n, float scale) {
+  for (size_t i = first + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dst[i] = src[i] / scale;
+}
+
+hipError_t launch_image_to_host(const float* src, float* dst, size_t n, float scale, hipStream_t s) {
+  const bool aligned = (((uintptr_t)src | (uintptr_t)dst) & 15u) == 0;
+  const size_t n4 = aligned ? n / 4 : 0;
+  if (n4) {
+    const size_t blocks = std::min<size_t>((n4 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_image_to_host, dim3((uint32_t)blocks), dim3(256), 0, s, reinterpret_cast<const float4*>(src),
+                       reinterpret_cast<float4*>(dst), n4, scale);
+  }
+  if (n4 * 4 < n) {
+    const size_t blocks = std::min<size_t>((n - n4 * 4 + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_image_to_host_scalar, dim3((uint32_t)blocks), dim3(256), 0, s, src, dst, n4 * 4, n, scale);
+  }
+  return hipGetLastError();
 }
 
 // ----------------------------------------------------------- cell table ---

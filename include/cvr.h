@@ -240,6 +240,12 @@ int cvr_clear_output(cvr_ctx* ctx);
 int cvr_get_stats(cvr_ctx* ctx, cvr_stats* stats);
 /* D->H copy of the tile buffer, every component divided by `scale`. */
 int cvr_copy_output(cvr_ctx* ctx, float* host_rgba, float scale);
+/* Extension, asynchronous on `stream` (a hipStream_t; NULL = the null
+ * stream): host_dst[i] = device_src[i] / scale for n_floats floats, written by
+ * a kernel straight into pinned (hipHostMalloc) or registered (hipHostRegister)
+ * host memory: the transfer delegate's Scale + D->H copy
+ * (ImageBufferTransfer.cu:61-78) in stream order, with no copy engine. */
+int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats, float scale, void* stream);
 /* Debug/parity: trace path ids [first, first+count) one per work-item and
  * return per-path records (no framebuffer splat). */
 int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_record* host_out);

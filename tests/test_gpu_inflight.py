@@ -176,3 +176,30 @@ def test_morton_sorted_track_order_vs_oracle(cvr, oracle_mod, name):
     assert_counters_equal(s1, rst, "morton vs oracle")
     assert_pixels_close(i1, ref, ITERS, "morton vs oracle")
     assert_pixels_close(i1, i0, ITERS, "morton vs unsorted")
+
+
+def test_image_to_host_matches_division(cvr):
+    """cvr_image_to_host: the kernel's x / scale into pinned memory equals
+    IEEE fp32 division, including a ragged tail and an unaligned interior
+    offset.  (HIP through ctypes: in this process libcvr loaded the HIP
+    runtime before torch could.)"""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so.7")
+    P = C.c_void_p
+    rng = np.random.default_rng(3)
+    for n in (1, 7, 4096, (1 << 20) | 3):
+        a = (rng.standard_normal(n) * 1e3).astype(np.float32)
+        d_src, h_buf = P(), P()
+        assert hip.hipMalloc(C.byref(d_src), C.c_size_t(n * 4)) == 0
+        assert hip.hipHostMalloc(C.byref(h_buf), C.c_size_t((n + 8) * 4), 0) == 0
+        try:
+            assert hip.hipMemcpy(d_src, a.ctypes.data_as(P), C.c_size_t(n * 4), 1) == 0  # H2D
+            host = np.ctypeslib.as_array(C.cast(h_buf, C.POINTER(C.c_float)), shape=(n + 8,))
+            host[:] = 0
+            cvr._lib.image_to_host(d_src.value, h_buf.value + 20, n, 20.0, None)  # 5 floats in: unaligned
+            assert hip.hipDeviceSynchronize() == 0
+            assert np.array_equal(host[5:5 + n], a / np.float32(20.0))
+            assert (host[:5] == 0).all() and (host[5 + n:] == 0).all()
+        finally:
+            hip.hipFree(d_src)
+            hip.hipHostFree(h_buf)
