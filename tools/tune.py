@@ -111,16 +111,17 @@ def main():
             wall = (time.perf_counter() - t0) * 1e3
             if r > 0:
                 times[v].append(wall)
-                extra[v] = (st.kernel_ms, st.iterations, st.track_ms, st.events_ms, st.steps, st.escaped, st.fetches)
+                extra[v] = (st.kernel_ms, st.iterations, st.track_ms, st.events_ms, st.steps, st.escaped, st.fetches,
+                            st.density)
     cu, grid = ctxs[-1][1].device_info()
     print(f"CUs {cu}, persistent grid {grid} blocks; steps/launch {st.steps}, density {st.density}")
     for v, _ in ctxs:
         t = np.array(times[v])
-        kms, its, tms, ems, steps, esc, fetches = extra[v]
+        kms, its, tms, ems, steps, esc, fetches, dens = extra[v]
         gsteps = steps / (np.median(t) * 1e-3) / 1e9
         print(f"{v:42s} wall {np.median(t):8.3f} ms (min {t.min():7.3f}) dev {kms:8.3f}  it {its:4d} "
               f"track {tms:7.3f} events {ems:7.3f}  {W * H * a.iters / np.median(t) / 1e3:7.1f} Msamples/s "
-              f"{gsteps:6.2f} Gsteps/s  esc {esc} fetch {fetches / max(st.density, 1):.3f}", flush=True)
+              f"{gsteps:6.2f} Gsteps/s  esc {esc} fetch {fetches / max(dens, 1):.3f}", flush=True)
 
 
 if __name__ == "__main__":
