@@ -75,7 +75,8 @@ typedef enum {
   CVR_OPT_WAVES = 10,         /* register/LDS budget in waves per SIMD: persistent kernel 4 (default), 5, 6,
                                  8; wave-pool kernel 3, 4, 5, 6 (default: 5 dense, 4 sparse; 6 is dense only
                                  and spills) */
-  CVR_OPT_ORDER = 11,         /* 1 (default): 8x8-pixel blocks, samples innermost; 0: path-id order */
+  CVR_OPT_ORDER = 11,         /* 2 (default): 8x8-pixel blocks, samples innermost, each XCD band's blocks in
+                                 2-D Morton order; 1: the same blocks row-major; 0: path-id order */
   CVR_OPT_QUEUES = 12,        /* work bands / queues, one per XCD (default 8) */
   CVR_OPT_BOUNDS = 13,        /* brick bounds: log2 brick size 1..5, 0 = off (default 2 dense,
                                  3 sparse; sparse caps at 3); next cvr_set_medium.  Results are

@@ -24,6 +24,9 @@ def block_costs(ctx, W, H, samples=1, w_seg=8.0):
     return np.bincount(b, weights=cost, minlength=(W // 8) * (H // 8))
 
 
+ctx_blocks_x = [0]
+
+
 def order(ctx, tile_cost, rank, world, how, rng):
     nb, nq, qbeg = ctx.launch_blocks()
     local_cost = tile_cost[rank + world * np.arange(nb)]
@@ -37,6 +40,14 @@ def order(ctx, tile_cost, rank, world, how, rng):
             idx = idx[np.argsort(local_cost[a:e], kind="stable")]
         elif how == "random":
             idx = rng.permutation(idx)
+        elif how == "zorder":  # 2-D Morton order of the band's blocks (compact in-flight footprint)
+            bx_n = ctx_blocks_x[0]
+            tb = rank + world * idx  # tile block ids
+            bx, by = tb % bx_n, tb // bx_n
+            code = np.zeros(len(idx), np.int64)
+            for bit in range(16):
+                code |= ((bx >> bit) & 1) << (2 * bit) | ((by >> bit) & 1) << (2 * bit + 1)
+            idx = idx[np.argsort(code, kind="stable")]
         perm[a:e] = idx
     return perm
 
@@ -48,6 +59,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--shards", type=int, nargs="*", default=[1, 8])
+    ap.add_argument("--orders", nargs="*", default=["natural", "desc", "asc", "random", "zorder"])
     a = ap.parse_args()
     scene = cvr.Scene.synthetic(a.scene)
     W = H = a.res
@@ -65,7 +77,8 @@ def main():
     for world in a.shards:
         c.set_path_range(0, W * H * a.iters)
         c.set_block_shard(0, world)
-        perms = {h: order(c, cost, 0, world, h, rng) for h in ("natural", "desc", "asc", "random")}
+        ctx_blocks_x[0] = W // 8
+        perms = {h: order(c, cost, 0, world, h, rng) for h in a.orders}
         times = {h: [] for h in perms}
         ref = None
         for r in range(a.rounds + 1):
