@@ -193,7 +193,7 @@ class HostImage:
                     pass
 
 
-KERNEL_COPY_MAX_BYTES = 4 << 20
+KERNEL_COPY_MAX_BYTES = int(os.environ.get("CVR_KERNEL_COPY_MAX_BYTES", 4 << 20))
 
 
 def reduce_to_host(acc_flat, part, host: HostImage, scale: float, dist):
