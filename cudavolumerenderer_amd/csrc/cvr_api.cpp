@@ -1092,12 +1092,13 @@ int cvr_launch_render(cvr_ctx* c) {
   fill_launch(c, L, first, count);
   if ((r = ensure_zorder(c, L))) return r;
   const bool eps = scatter_eps_for(c);
-  if (!c->chunk && scheduler_for(c) == 3 && !c->grid_override) {
+  if (!c->chunk && scheduler_for(c) == 3) {
     // Wave-pool dequeue chunk by the paths each wave gets: about 8 chunks per
     // wave, 64..256 paths.  Small launches (block shards of a multi-GPU render)
     // then end with the waves' last chunks evenly spread (C2 shard 1/8 on one
     // GPU: 1.09 ms at 64 vs 1.18 at 256; the whole C2 launch keeps 256).
-    const uint64_t grid = (uint64_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
+    const uint64_t grid =
+        c->grid_override ? (uint64_t)c->grid_override : (uint64_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
     const uint64_t per_wave = grid ? (uint64_t)L.path_count / grid : 0;
     L.chunk = per_wave >= 2048 ? 256u : per_wave >= 1024 ? 128u : 64u;
   }

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--shard", type=int, default=1)
+    ap.add_argument("--grid", type=int, default=0, help="wave-pool workgroups per launch (0: full occupancy)")
     a = ap.parse_args()
     scene = cvr.Scene.synthetic(a.scene)
     W = H = a.res
@@ -33,6 +34,8 @@ def main():
         else:
             c.set_medium(scene.medium)
         c.set_camera(iv, r2v, (W, H))
+        if a.grid:
+            c.set_option(cvr.OPT_GRID, a.grid)
         c.init()
         c.use_own_stream()
         c.set_resolution(W, H)
