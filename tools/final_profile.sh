@@ -19,6 +19,7 @@ step() {  # name seconds cmd...
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
 }
 B="python3 bench.py --no-cpu-baseline"
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 600 python3 -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider
 step c2_bench 200 python3 bench.py --steps 20 --warmup 5
 step c1_bench 200 python3 bench.py --scene bucky --steps 20 --warmup 5
