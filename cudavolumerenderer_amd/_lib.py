@@ -111,6 +111,7 @@ def load() -> C.CDLL:
         "cvr_set_block_shard": (I32, [P, U32, U32]),
         "cvr_set_block_order": (I32, [P, P, U32]),
         "cvr_share_medium": (I32, [P, P]),
+        "cvr_trace_launch": (I32, [P, P, U64]),
         "cvr_image_to_host": (I32, [P, P, C.c_size_t, C.c_float, P]),
         "cvr_launch_blocks": (I32, [P, P, P, P]),
         "cvr_set_seed": (I32, [P, U32]),
@@ -441,6 +442,13 @@ class Context:
         out = np.zeros(count, PATH_RECORD_DTYPE)
         self._c(load().cvr_trace_paths(self._h, first, count,
                                        out.ctypes.data_as(C.POINTER(PathRecord))))
+        return out
+
+    def trace_launch(self, n: int) -> np.ndarray:
+        """The production wave-pool launch of the current range (n path ids)
+        with per-path final records (cvr_trace_launch)."""
+        out = np.zeros(n, PATH_RECORD_DTYPE)
+        self._c(load().cvr_trace_launch(self._h, out.ctypes.data_as(C.POINTER(PathRecord)), n))
         return out
 
     def device_info(self):

@@ -82,6 +82,7 @@ struct cvr_ctx {
   uint32_t* d_sbounds = nullptr;
   uint32_t* d_scoarse = nullptr;
   uint32_t* d_block_perm = nullptr;  // cvr_set_block_order
+  void* d_rec_active = nullptr;      // cvr_trace_launch: records of the launch in progress
   uint32_t block_perm_n = 0;
   size_t n_cell_leaves = 0;  // cell-leaf pool slots (incl. the zero slot)
   bool have_medium = false;
@@ -1152,6 +1153,7 @@ int cvr_launch_render(cvr_ctx* c) {
       c->pool_T_n = need;
     }
     L.pool_T = c->d_pool_T;
+    L.rec = c->d_rec_active;
     HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, waves, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
@@ -1250,6 +1252,40 @@ int cvr_copy_output(cvr_ctx* c, float* host, float scale) {
   HIP_TRY(c, hipMemcpy(host, c->d_out, n * sizeof(float), hipMemcpyDeviceToHost));
   if (scale != 1.0f)
     for (size_t i = 0; i < n; ++i) host[i] = host[i] / scale;
+  return CVR_OK;
+}
+
+int cvr_trace_launch(cvr_ctx* c, cvr_path_record* out, uint64_t n_out) {
+  if (!c || !out) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  int r = check_ready(c);
+  if (r) return r;
+  if ((r = do_init(c))) return r;
+  if (scheduler_for(c) != 3 || c->rng_binding || c->kernel == CVR_KERNEL_NAIVE_SK || c->kernel == CVR_KERNEL_NAIVE_MK)
+    return set_err(&c->err, CVR_ERR_UNSUPPORTED, "cvr_trace_launch traces the wave-pool scheduler only");
+  uint64_t first, count;
+  compute_range(c, &first, &count);
+  if (n_out != count)
+    return set_err(&c->err, CVR_ERR_INVALID, "record buffer holds %llu records, the launch range %llu",
+                   (unsigned long long)n_out, (unsigned long long)count);
+  const bool sparse = c->m.leaves != nullptr;
+  const uint64_t grid = c->grid_override ? c->grid_override : (uint64_t)(sparse ? c->wpool_grid_sparse : c->wpool_grid);
+  const size_t pid_bytes = (size_t)grid * cvr::wpool_slots(wpool_waves_for(c, sparse), sparse) * sizeof(uint32_t);
+  const size_t rec_bytes = (size_t)count * sizeof(cvr_path_record);
+  char* d = nullptr;
+  HIP_TRY(c, hipMalloc(&d, pid_bytes + rec_bytes + 16));
+  hipError_t e = hipMemsetAsync(d, 0, pid_bytes + rec_bytes + 16, c->stream);
+  if (e == hipSuccess) {
+    c->d_rec_active = d + pid_bytes;
+    r = cvr_launch_render(c);
+    c->d_rec_active = nullptr;
+    if (!r) {
+      e = hipStreamSynchronize(c->stream);
+      if (e == hipSuccess) e = hipMemcpy(out, d + pid_bytes, rec_bytes, hipMemcpyDeviceToHost);
+    }
+  }
+  (void)hipFree(d);
+  if (r) return r;
+  if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "trace launch: %s", hipGetErrorString(e));
   return CVR_OK;
 }
 

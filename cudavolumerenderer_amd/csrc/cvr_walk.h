@@ -179,6 +179,10 @@ struct LaunchParams {
   unsigned int* queue;    // work-queue heads, one per 64-byte line (zeroed per launch)
   unsigned long long* stats;  // CVR_STAT_* counters (zeroed per launch)
   float4* pool_T;         // wave-pool scheduler: event-only slot part, grid * slots float4 (cvr_api wpool_slots)
+  // Debug (cvr_trace_launch): the wave pool writes each path's final record
+  // (cvr_path_record) at rec[path_id - path_first]; a u32 path-id array of
+  // grid * slots entries sits just below rec.  Null in production.
+  void* rec;
   uint32_t chunk;         // paths per wave dequeue
   uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
   uint32_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track

@@ -171,6 +171,28 @@ __device__ __forceinline__ void load_track(const WavePool<kSlots, kSplit>& S, ui
 enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
 
 // The wave's path cursor into the global work queues (as k_persistent).
+// Debug records (LaunchParams::rec): a path's final state when it ends, in
+// the oracle's per-path record layout (cvr_kernels.h PathRecord; steps and
+// density counts are per lane here, so they stay 0).
+template <int kSlots>
+__device__ __forceinline__ uint32_t* rec_pids(const LaunchParams& L) {
+  // the path-id array (grid * slots u32) sits just below the records
+  return reinterpret_cast<uint32_t*>(L.rec) - (size_t)gridDim.x * kSlots + (size_t)blockIdx.x * kSlots;
+}
+template <int kSlots>
+__device__ __forceinline__ void record_end(const LaunchParams& L, uint32_t s, const PathState& ps, uint32_t flags,
+                                           uint32_t nseg) {
+  const uint32_t pid = rec_pids<kSlots>(L)[s];
+  PathRecord r = {};
+  r.image_id = ps.image_id;
+  r.flags = flags;
+  r.T[0] = ps.T.x;
+  r.T[1] = ps.T.y;
+  r.T[2] = ps.T.z;
+  r.n_segments = nseg;
+  static_cast<PathRecord*>(L.rec)[pid - L.path_first] = r;
+}
+
 struct Cursor {
   uint32_t next, end, q, home;
   bool exhausted;
@@ -178,7 +200,7 @@ struct Cursor {
 
 }  // namespace
 
-template <bool kScatterEps, int kWaves, bool kSparse>
+template <bool kScatterEps, int kWaves, bool kSparse, bool kRecord>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr bool kSplit = !kSparse || CVR_WPOOL_SPLIT_SPARSE;
   constexpr int kSlots = PoolSize<kWaves, kSplit>::value;
@@ -452,7 +474,9 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           }
           const uint32_t take = min((uint32_t)__popcll(want) - given, cur.end - cur.next);
           if (kind == K_NEW && rank >= given && rank < given + take) {
-            path_begin(L, unit_to_path(L, cur.q, cur.next + (rank - given)), ps);
+            const uint32_t pid = unit_to_path(L, cur.q, cur.next + (rank - given));
+            path_begin(L, pid, ps);
+            if (kRecord) rec_pids<kSlots>(L)[s] = pid;
             is.normal = mk3(0, 0, 0);
             nseg = 0;
             got = true;
@@ -468,6 +492,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           if (L.max_segments && nseg >= L.max_segments) {
             truncated = true;
             to_ln = true;
+            if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);
           } else {
             ++nseg;
             seg_first = true;
@@ -475,6 +500,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
               splat(L, ps);
               escaped = true;
               to_ln = true;
+              if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
             } else if (is.inside) {
               store_full(S, L.pool_T + (size_t)blockIdx.x * kSlots, s, ps, is, nseg);
               to_ready = true;
@@ -510,12 +536,16 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       CVR_LAP(8)
 #endif
       const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
-      if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) to_ln = true;  // the path died in roulette
+      if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {  // the path died in roulette
+        to_ln = true;
+        if (kRecord) record_end<kSlots>(L, s, ps, 0u, nseg);
+      }
       // ---- next segment: AABB test of the survivors ----------------------
       if (alive) {
         if (L.max_segments && nseg >= L.max_segments) {
           truncated = true;
           to_ln = true;
+          if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);
         } else {
           ++nseg;
           seg_next = true;
@@ -523,6 +553,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             splat(L, ps);
             escaped = true;
             to_ln = true;
+            if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
           } else {
             store_full(S, gT, s, ps, is, nseg);
             to_ready = is.inside;  // medium: Woodcock from t = 0
@@ -588,19 +619,28 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
 template <bool E>
 static const void* wpool_fn(int waves, bool sparse) {
-  if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true>)
-                                 : reinterpret_cast<const void*>(&k_wpool<E, 4, true>);
-  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false>);
-  if (waves == 6) return reinterpret_cast<const void*>(&k_wpool<E, 6, false>);
-  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false>);
-  return reinterpret_cast<const void*>(&k_wpool<E, 4, false>);
+  if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, false>)
+                                 : reinterpret_cast<const void*>(&k_wpool<E, 4, true, false>);
+  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false, false>);
+  if (waves == 6) return reinterpret_cast<const void*>(&k_wpool<E, 6, false, false>);
+  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false, false>);
+  return reinterpret_cast<const void*>(&k_wpool<E, 4, false, false>);
+}
+// Record instances (cvr_trace_launch; debug only, so the production kernels
+// carry none of the record code): the default register budgets.
+template <bool E>
+static const void* wpool_record_fn(int waves, bool sparse) {
+  if (sparse) return waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, true, true>) : nullptr;
+  return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, false, true>) : nullptr;
 }
 
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
                         hipStream_t s) {
   if (L.path_count == 0) return hipSuccess;
   const bool sparse = m.leaves != nullptr;
-  const void* fn = scatter_eps ? wpool_fn<true>(waves, sparse) : wpool_fn<false>(waves, sparse);
+  const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
+                         : (scatter_eps ? wpool_fn<true>(waves, sparse) : wpool_fn<false>(waves, sparse));
+  if (!fn) return hipErrorInvalidValue;  // no record instance for this register budget
   MediumParams mm = m;
   LaunchParams ll = L;
   void* args[] = {&mm, &ll};

@@ -250,6 +250,14 @@ int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats,
 /* Debug/parity: trace path ids [first, first+count) one per work-item and
  * return per-path records (no framebuffer splat). */
 int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_record* host_out);
+/* Debug: the production launch (cvr_launch_render on the wave-pool scheduler,
+ * regenerationSK / sortingSK) writing every path's final record as it ends:
+ * out[p - first] for the path ids p of the launch range [first, first + n_out)
+ * (cvr_set_path_range; n_out must equal the range's length).  image_id, flags,
+ * T and n_segments are filled (n_steps, n_density, n_albedo stay 0: the wave
+ * pool counts those per lane); ids outside a block shard stay zero.
+ * Synchronous. */
+int cvr_trace_launch(cvr_ctx* ctx, cvr_path_record* out, uint64_t n_out);
 /* Diagnostic builds (-DCVR_STAMPS=1) only: per-phase cycle counters of the
  * persistent kernel {event cycles, track cycles, event phases, track
  * iterations}, summed over waves; zeros otherwise. */

@@ -1,0 +1,133 @@
+"""Per-path bit-exact parity of the production kernel itself.
+
+cvr_trace_launch runs the benchmark's launch (regenerationSK / sortingSK on
+the wave-pool scheduler, k_wpool's dense and sparse instances, pixel-block
+work order, every scheduling knob at its default) and has each path write its
+final record when it ends.  Every path's image id, end flags (escaped /
+truncated / roulette), throughput T bits and segment count must equal the
+oracle's trace of the same path id (oracle/cvr_oracle.c: the reference's
+RegenerationVolPTsk / NaiveVolPTsk walk, RegenerationVolPTsk_kernel.cuh:146-232,
+NaiveVolPTsk_kernel.cuh:17-87)."""
+import os
+
+import numpy as np
+import pytest
+
+from parity_util import TILE_SEED, oracle_for_scene
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _ctx(cvr, scene, W, H, kernel="regenerationSK", iv=None, r2v=None):
+    ctx = cvr.Context(0, kernel)
+    if scene.is_sparse:
+        ctx.set_medium_sparse(scene.sparse_medium)
+    else:
+        ctx.set_medium(scene.medium)
+    if iv is None:
+        iv, r2v = cvr.default_camera(W, H)
+    ctx.set_camera(iv, r2v, (W, H))
+    ctx.init()
+    return ctx, iv, r2v
+
+
+def _compare(g, c, what):
+    assert len(g) == len(c)
+    for f in ("image_id", "flags", "n_segments"):
+        mism = np.nonzero(g[f] != c[f])[0]
+        assert mism.size == 0, f"{what}: {f} differs for {mism.size} paths, first {mism[:5]}"
+    tb, cb = g["T"].view(np.uint32), c["T"].view(np.uint32)
+    both_nan = np.isnan(g["T"]) & np.isnan(c["T"])
+    mism = np.nonzero(((tb != cb) & ~both_nan).any(axis=1))[0]
+    assert mism.size == 0, f"{what}: T bits differ for {mism.size} paths, first {mism[:5]}"
+    assert (c["flags"] & 1).any() and (c["flags"] == 0).any(), what  # escapes and roulette deaths
+
+
+def _launch_vs_oracle(ctx, orc, iv, r2v, full, tile, offset, iters, seed, first, count, kid, what):
+    ctx.set_resolution(*tile)
+    ctx.set_offset(*offset)
+    ctx.set_iterations(iters)
+    ctx.set_seed(seed)
+    ctx.set_path_range(first, count)
+    g = ctx.trace_launch(count)
+    L = orc.launch(iv, r2v, full, tile, offset, kid, seed)
+    c = orc.trace_paths(L, first, count)
+    _compare(g, c, what)
+    return g
+
+
+@pytest.mark.parametrize("kernel", ["regenerationSK", "sortingSK"])
+@pytest.mark.parametrize("name", ["manix", "hetvol", "bucky"])
+def test_production_launch_per_path_bit_exact(cvr, oracle_mod, name, kernel):
+    scene = cvr.Scene.synthetic(name)
+    W = H = 256
+    iters = 4
+    ctx, iv, r2v = _ctx(cvr, scene, W, H, kernel)
+    orc = oracle_for_scene(oracle_mod, scene)
+    kid = cvr.KERNELS.index(kernel)
+    _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), iters, 0, 0, W * H * iters, kid, f"{name} {kernel}")
+
+
+def test_production_launch_records_c2_sample_and_shard(cvr, oracle_mod):
+    """C2 (1024^2, 20 it): two whole samples in the benchmark's work order,
+    then block shard 5 of 8 of all 20 samples (the per-rank launch of an
+    8-GPU render): every launched path bit-exact, the others untouched."""
+    from cudavolumerenderer_amd.distributed import block_shard_path_ids
+    scene = cvr.Scene.synthetic("manix")
+    W = H = 1024
+    P = W * H
+    ctx, iv, r2v = _ctx(cvr, scene, W, H)
+    orc = oracle_for_scene(oracle_mod, scene)
+    _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 20, 0, 7 * P, 2 * P, 2, "C2 samples 7-8")
+    ctx.set_iterations(20)
+    ctx.set_path_range(0, 20 * P)
+    ctx.set_block_shard(5, 8)
+    g = ctx.trace_launch(20 * P)
+    ids = block_shard_path_ids(W, H, 20, 5, 8)
+    mask = np.zeros(20 * P, bool)
+    mask[ids] = True
+    assert (g["n_segments"][~mask] == 0).all()
+    sel = ids[::97]  # a spread sample of the shard's paths, traced one by one by the oracle
+    L = orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 2, 0)
+    c = np.concatenate([orc.trace_paths(L, int(p), 1) for p in sel])
+    _compare(g[sel], c, "C2 shard 5/8")
+
+
+def test_production_launch_records_c4_tiles(cvr, oracle_mod):
+    """C4 (2048^2, 256 it, 4x2 tiles): a 2-sample range of every tile with
+    that tile's regenerationSK seed (+n_paths per tile)."""
+    scene = cvr.Scene.synthetic("manix")
+    W = H = 2048
+    tw, th = W // 4, H // 2
+    P = tw * th
+    iters = 256
+    ctx, iv, r2v = _ctx(cvr, scene, W, H)
+    orc = oracle_for_scene(oracle_mod, scene)
+    for k in range(8):
+        off = (tw * (k % 4), th * (k // 4))
+        s0 = (53 * k + 5) % (iters - 2)
+        _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (tw, th), off, iters, TILE_SEED[2](0, k, P * iters),
+                          s0 * P, 2 * P, 2, f"C4 tile {k}")
+
+
+def test_production_launch_records_c5_sparse(cvr, oracle_mod):
+    """C5 (sparse cloud, 4096^2, 20 it): 2 M path ids of sample 11 through
+    k_wpool's sparse instance (an unaligned range: path-id work order)."""
+    scene = cvr.Scene.synthetic("cloud")
+    W = H = 4096
+    ctx, iv, r2v = _ctx(cvr, scene, W, H)
+    orc = oracle_for_scene(oracle_mod, scene)
+    _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 20, 0, 11 * W * H + 123457, 2 << 20, 2,
+                      "C5 sample 11")
+
+
+def test_production_launch_records_bonsai_vdb(cvr, oracle_mod):
+    """The reference's bonsai_small.vdb (real data) with its scene camera."""
+    scene = cvr.Scene.load(os.path.join(GOLDEN, "bonsai_small.vdb"))
+    W = H = 512
+    iv, r2v = scene.camera(W, H)
+    ctx, _, _ = _ctx(cvr, scene, W, H, "regenerationSK", iv, r2v)
+    orc = oracle_for_scene(oracle_mod, scene)
+    _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 4, 0, 0, W * H * 4, 2, "bonsai")
