@@ -180,11 +180,14 @@ def _write_vol(path, data_zyxc, bbox):
 
 @pytest.fixture(scope="module")
 def xml_scene(cvr, tmp_path_factory):
+    return make_xml_scene(cvr, tmp_path_factory.mktemp("xml"))
+
+
+def make_xml_scene(cvr, d):
     """hetvol.xml (the reference's smoke scene) re-pointed at generated .vol
-    files: density box (-1,-2,-3)-(1,2,3), albedo box (-0.3,-0.2,-0.4)-(0.5,0.4,0.8);
-    the scene AABB is the albedo's (Q15) and densities reach 1.6 > the capped
-    majorant 1."""
-    d = tmp_path_factory.mktemp("xml")
+    files in directory `d`: density box (-1,-2,-3)-(1,2,3), albedo box
+    (-0.3,-0.2,-0.4)-(0.5,0.4,0.8); the scene AABB is the albedo's (Q15) and
+    densities reach 1.6 > the capped majorant 1."""
     rng = np.random.default_rng(23)
     nz, ny, nx = 24, 20, 28
     z, y, x = np.meshgrid(np.linspace(-1, 1, nz), np.linspace(-1, 1, ny), np.linspace(-1, 1, nx), indexing="ij")

@@ -131,3 +131,26 @@ def test_production_launch_records_bonsai_vdb(cvr, oracle_mod):
     ctx, _, _ = _ctx(cvr, scene, W, H, "regenerationSK", iv, r2v)
     orc = oracle_for_scene(oracle_mod, scene)
     _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 4, 0, 0, W * H * 4, 2, "bonsai")
+
+
+def test_production_launch_records_mhd_and_xml(cvr, oracle_mod, tmp_path):
+    """Scenes through the MHD loader (convert-mhd semantics) and the Mitsuba
+    XML loader with non-unit .vol boxes (quirks Q4 and Q15 change the walk),
+    per path through the production launch."""
+    import test_gpu_production as tp
+    rng = np.random.default_rng(11)
+    nz, ny, nx = 56, 40, 48
+    z, y, x = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    r = np.sqrt(((x - 23) / 20.0) ** 2 + ((y - 19) / 16.0) ** 2 + ((z - 27) / 24.0) ** 2)
+    img = np.clip(1500 * (1.1 - r) + rng.normal(0, 80, r.shape), -1000, 3000).round()
+    tp._write_mhd(str(tmp_path / "ct.mhd"), img)
+    mhd = cvr.Scene.load(str(tmp_path / "ct.mhd"))
+    (tmp_path / "xml").mkdir()
+    xml = tp.make_xml_scene(cvr, tmp_path / "xml")
+    assert not np.allclose(np.array(xml.medium.box_max) - np.array(xml.medium.box_min), 1.0)
+    for name, scene in (("mhd", mhd), ("xml", xml)):
+        W = H = 256
+        iv, r2v = scene.camera(W, H)
+        ctx, _, _ = _ctx(cvr, scene, W, H, "regenerationSK", iv, r2v)
+        orc = oracle_for_scene(oracle_mod, scene)
+        _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 4, 3, 0, W * H * 4, 2, name)
