@@ -27,7 +27,7 @@ def main():
     W = H = a.res
     iv, r2v = cvr.default_camera(W, H)
     ctxs = []
-    for _ in range(3):
+    for _ in range(4):
         c = cvr.Context(0, "regenerationSK")
         if scene.is_sparse:
             c.set_medium_sparse(scene.sparse_medium)
@@ -61,7 +61,8 @@ def main():
         r1 = run(ctxs[:1], a.steps)
         r2 = run(ctxs[:2], a.steps)
         r3 = run(ctxs[:3], a.steps)
-        print(f"round {rnd}: one context {r1:.3f} ms/render, two alternating {r2:.3f}, three {r3:.3f} "
+        r4 = run(ctxs[:4], a.steps)
+        print(f"round {rnd}: one context {r1:.3f} ms/render, two alternating {r2:.3f}, three {r3:.3f}, four {r4:.3f} "
               f"({W * H * a.iters / a.shard / r1 / 1e3:.0f} / {W * H * a.iters / a.shard / r2 / 1e3:.0f} / "
               f"{W * H * a.iters / a.shard / r3 / 1e3:.0f} Msamples/s)", flush=True)
 
