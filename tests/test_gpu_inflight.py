@@ -203,3 +203,34 @@ def test_image_to_host_matches_division(cvr):
         finally:
             hip.hipFree(d_src)
             hip.hipHostFree(h_buf)
+
+
+def test_shared_sparse_medium_in_flight(cvr):
+    """A small sparse cloud (leaves, cell-leaf pool, brick words) shared by a
+    second context on its own stream: both launched back to back without a
+    sync render the same counters and pixels."""
+    from test_sparse import CLOUD_SMALL
+    scene = cvr.Scene.synthetic("cloud", 0, CLOUD_SMALL)
+    a = _owner(cvr, scene)
+    _setup(cvr, a)
+    b = cvr.Context(0, "regenerationSK")
+    b.share_medium(a)
+    _setup(cvr, b)
+    a.use_own_stream()
+    b.use_own_stream()
+    for c in (a, b):
+        c.clear_output()
+        c.launch_render()
+    ia, sa = c_out(a)
+    ib, sb = c_out(b)
+    for k in ("paths", "segments", "steps", "density", "albedo", "escaped", "fetches"):
+        assert getattr(sa, k) == getattr(sb, k), k
+    assert sa.fetches < sa.density and sa.albedo > 0
+    assert_pixels_close(ib, ia, ITERS, "shared sparse medium")
+    b.close()
+    a.close()
+
+
+def c_out(c):
+    c.synchronize()
+    return c.copy_output(W, H), c.stats()
