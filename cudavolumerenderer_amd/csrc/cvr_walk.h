@@ -413,15 +413,21 @@ struct WoodcockPoint {
 CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t) {
   WoodcockPoint P;
   P.c = sub3(mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z)), m.shift);
-  P.cx = P.c.x * m.gx;
-  P.cy = P.c.y * m.gy;
-  P.cz = P.c.z * m.gz;
+  // fma(c, g, +0) is the product c*g rounded once, except that a -0 product
+  // becomes +0 (-0 + +0 = +0); the trilinear weights cx - floor(cx) and the
+  // cell index are the same for both zeros.
+  P.cx = det_fmaf(P.c.x, m.gx, 0.0f);
+  P.cy = det_fmaf(P.c.y, m.gy, 0.0f);
+  P.cz = det_fmaf(P.c.z, m.gz, 0.0f);
   P.fx1 = __builtin_floorf(P.cx);
   P.fy1 = __builtin_floorf(P.cy);
   P.fz1 = __builtin_floorf(P.cz);
-  // bitwise &: one mask, no short-circuit branches; NaN fails every compare
-  P.in = (P.fx1 >= 0.0f) & (P.fx1 < m.fres_x) & (P.fy1 >= 0.0f) & (P.fy1 < m.fres_y) & (P.fz1 >= 0.0f) &
-         (P.fz1 < m.fres_z);
+  // floor(cx) >= 0 && floor(cx) < res  <=>  0 <= cx < res (res an integer)
+  // <=>  bits(cx) < bits(res) as unsigned: non-negative floats order as
+  // their bit patterns, negatives and -NaN have the sign bit set, +NaN lies
+  // above +inf, and cx is never -0 (above).  One compare per axis, one mask.
+  P.in = ((int)(det_f2u(P.cx) < det_f2u(m.fres_x)) & (int)(det_f2u(P.cy) < det_f2u(m.fres_y)) &
+          (int)(det_f2u(P.cz) < det_f2u(m.fres_z))) != 0;
   const uint32_t x1 = P.in ? (uint32_t)P.fx1 : 0u, y1 = P.in ? (uint32_t)P.fy1 : 0u,
                  z1 = P.in ? (uint32_t)P.fz1 : 0u;
   // 24-bit multiplies: the host keeps bnx*bny, rx*ry and ry*rz below 2^24
