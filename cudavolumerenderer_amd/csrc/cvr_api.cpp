@@ -1279,8 +1279,19 @@ int cvr_trace_launch(cvr_ctx* c, cvr_path_record* out, uint64_t n_out) {
     r = cvr_launch_render(c);
     c->d_rec_active = nullptr;
     if (!r) {
+      // the kernel writes path p's record at p - L.path_first: a contiguous
+      // shard (no block order) moved path_first to the shard's first id
+      cvr::LaunchParams Ls{};
+      fill_launch(c, Ls, first, count);
+      const uint64_t shift = Ls.path_first - first;
       e = hipStreamSynchronize(c->stream);
-      if (e == hipSuccess) e = hipMemcpy(out, d + pid_bytes, rec_bytes, hipMemcpyDeviceToHost);
+      if (e == hipSuccess && shift) {
+        memset(out, 0, rec_bytes);
+        e = hipMemcpy(out + shift, d + pid_bytes, (size_t)Ls.path_count * sizeof(cvr_path_record),
+                      hipMemcpyDeviceToHost);
+      } else if (e == hipSuccess) {
+        e = hipMemcpy(out, d + pid_bytes, rec_bytes, hipMemcpyDeviceToHost);
+      }
     }
   }
   (void)hipFree(d);

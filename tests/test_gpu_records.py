@@ -33,7 +33,7 @@ def _ctx(cvr, scene, W, H, kernel="regenerationSK", iv=None, r2v=None):
     return ctx, iv, r2v
 
 
-def _compare(g, c, what):
+def _compare(g, c, what, mixed=True):
     assert len(g) == len(c)
     for f in ("image_id", "flags", "n_segments"):
         mism = np.nonzero(g[f] != c[f])[0]
@@ -42,10 +42,11 @@ def _compare(g, c, what):
     both_nan = np.isnan(g["T"]) & np.isnan(c["T"])
     mism = np.nonzero(((tb != cb) & ~both_nan).any(axis=1))[0]
     assert mism.size == 0, f"{what}: T bits differ for {mism.size} paths, first {mism[:5]}"
-    assert (c["flags"] & 1).any() and (c["flags"] == 0).any(), what  # escapes and roulette deaths
+    if mixed:
+        assert (c["flags"] & 1).any() and (c["flags"] == 0).any(), what  # escapes and roulette deaths
 
 
-def _launch_vs_oracle(ctx, orc, iv, r2v, full, tile, offset, iters, seed, first, count, kid, what):
+def _launch_vs_oracle(ctx, orc, iv, r2v, full, tile, offset, iters, seed, first, count, kid, what, mixed=True):
     ctx.set_resolution(*tile)
     ctx.set_offset(*offset)
     ctx.set_iterations(iters)
@@ -54,7 +55,7 @@ def _launch_vs_oracle(ctx, orc, iv, r2v, full, tile, offset, iters, seed, first,
     g = ctx.trace_launch(count)
     L = orc.launch(iv, r2v, full, tile, offset, kid, seed)
     c = orc.trace_paths(L, first, count)
-    _compare(g, c, what)
+    _compare(g, c, what, mixed)
     return g
 
 
@@ -154,3 +155,55 @@ def test_production_launch_records_mhd_and_xml(cvr, oracle_mod, tmp_path):
         ctx, _, _ = _ctx(cvr, scene, W, H, "regenerationSK", iv, r2v)
         orc = oracle_for_scene(oracle_mod, scene)
         _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 4, 3, 0, W * H * 4, 2, name)
+
+
+def test_production_launch_records_ragged_and_tiny(cvr, oracle_mod):
+    """Edge shapes of the launch: image sides that are not multiples of the
+    8x8 pixel block (the work order falls back to path-id order), a ragged
+    tile at an offset, a contiguous shard of a ragged image, a shard whose
+    rank owns no block, a 1x1 image and an empty range."""
+    scene = cvr.Scene.synthetic("manix")
+    orc = oracle_for_scene(oracle_mod, scene)
+    kid = 2
+    # 100x60: 3 whole samples
+    W, H = 100, 60
+    ctx, iv, r2v = _ctx(cvr, scene, W, H)
+    _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 3, 0, 0, W * H * 3, kid, "100x60")
+    # an unaligned range of the same image (starts and ends mid-sample)
+    _launch_vs_oracle(ctx, orc, iv, r2v, (W, H), (W, H), (0, 0), 3, 5, 4321, 7777, kid, "100x60 mid-sample")
+    # contiguous shard 1 of 3 of the ragged image: its third of the ids, the rest untouched
+    n = W * H * 3
+    ctx.set_resolution(W, H)
+    ctx.set_offset(0, 0)
+    ctx.set_seed(0)
+    ctx.set_path_range(0, n)
+    ctx.set_block_shard(1, 3)
+    g = ctx.trace_launch(n)
+    ctx.set_block_shard(0, 1)
+    lo, hi = n // 3, 2 * n // 3
+    assert (g["n_segments"][:lo] == 0).all() and (g["n_segments"][hi:] == 0).all()
+    L = orc.launch(iv, r2v, (W, H), (W, H), (0, 0), kid, 0)
+    _compare(g[lo:hi], orc.trace_paths(L, lo, hi - lo), "100x60 shard 1/3")
+    # a ragged 37x23 tile at (50, 30) of a 131x77 image
+    W2, H2 = 131, 77
+    ctx2, iv2, r2v2 = _ctx(cvr, scene, W2, H2)
+    _launch_vs_oracle(ctx2, orc, iv2, r2v2, (W2, H2), (37, 23), (50, 30), 4, 9, 0, 37 * 23 * 4, kid, "tile 37x23")
+    # 8x8 image = one pixel block: shard 1 of 3 owns no block and launches nothing
+    ctx3, iv3, r2v3 = _ctx(cvr, scene, 8, 8)
+    ctx3.set_resolution(8, 8)
+    ctx3.set_iterations(2)
+    ctx3.set_seed(0)
+    ctx3.set_path_range(0, 128)
+    ctx3.set_block_shard(1, 3)
+    g = ctx3.trace_launch(128)
+    assert (g["n_segments"] == 0).all()
+    ctx3.set_block_shard(0, 3)
+    g = ctx3.trace_launch(128)
+    L3 = orc.launch(iv3, r2v3, (8, 8), (8, 8), (0, 0), kid, 0)
+    _compare(g, orc.trace_paths(L3, 0, 128), "8x8 shard 0/3", mixed=False)
+    # 1x1 image, 64 samples, then an empty range
+    ctx4, iv4, r2v4 = _ctx(cvr, scene, 1, 1)
+    g = _launch_vs_oracle(ctx4, orc, iv4, r2v4, (1, 1), (1, 1), (0, 0), 64, 0, 0, 64, kid, "1x1", mixed=False)
+    assert (g["image_id"] == 0).all()
+    ctx4.set_path_range(0, 0)
+    assert ctx4.trace_launch(0).size == 0
