@@ -106,6 +106,22 @@ def render_tile_paths_sharded(render_tiles_range: Callable[[int, int], "object"]
     return img
 
 
+def init_process_group(dist, backend: str, device=None):
+    """One process per GPU: the node's ranks over RCCL ("nccl" on ROCm, one
+    device each) or gloo.  RCCL's collectives run on a high-priority stream:
+    the renders in flight keep every CU busy with persistent wave pools, so
+    the reduce-scatter's workgroups should be dispatched ahead of the next
+    render's as CU slots free up (the same reason the copy stream is high
+    priority in bench.py)."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        dist.init_process_group("nccl", device_id=device, pg_options=opts)
+    else:
+        dist.init_process_group("gloo")
+
+
 def block_shard_path_ids(tile_w: int, tile_h: int, samples: int, rank: int, world: int, first_sample: int = 0):
     """Path ids rank `rank` renders under cvr_set_block_shard(rank, world) for
     a launch of samples [first_sample, first_sample + samples) of a tile whose
