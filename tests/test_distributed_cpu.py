@@ -242,9 +242,10 @@ def test_block_shards_partition_path_ids(tw, th, samples, world):
 
 
 def _block_worker(rank, world, port, outdir):
-    from cudavolumerenderer_amd.distributed import HostImage, block_shard_path_ids, reduce_to_host
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from cudavolumerenderer_amd.distributed import HostImage, block_shard_path_ids, init_process_group, reduce_to_host
+    # bench.py's process-group init (env rendezvous, as under torch.distributed.run)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    init_process_group(dist, "gloo")
     try:
         orc, L = _scene_and_launch()
         n = W * H * 4
