@@ -22,16 +22,20 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--shard", type=int, default=1)
     ap.add_argument("--grid", type=int, default=0, help="wave-pool workgroups per launch (0: full occupancy)")
+    ap.add_argument("--contexts", type=int, nargs="*", default=[1, 2, 3, 4], help="renders in flight to time")
+    ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
     scene = cvr.Scene.synthetic(a.scene)
     W = H = a.res
     iv, r2v = cvr.default_camera(W, H)
     ctxs = []
-    for _ in range(4):
+    for k in range(max(a.contexts)):
         c = cvr.Context(0, "regenerationSK")
-        if scene.is_sparse:
+        if k:
+            c.share_medium(ctxs[0])
+        elif scene.is_sparse:
             c.set_medium_sparse(scene.sparse_medium)
-        else:
+        elif k == 0:
             c.set_medium(scene.medium)
         c.set_camera(iv, r2v, (W, H))
         if a.grid:
@@ -57,15 +61,12 @@ def main():
             c.synchronize()
         return (time.perf_counter() - t0) / steps * 1e3
 
-    for rnd in range(3):
-        r1 = run(ctxs[:1], a.steps)
-        r2 = run(ctxs[:2], a.steps)
-        r3 = run(ctxs[:3], a.steps)
-        r4 = run(ctxs[:4], a.steps)
-        print(f"round {rnd}: one context {r1:.3f} ms/render, two alternating {r2:.3f}, three {r3:.3f}, four {r4:.3f} "
-              f"({W * H * a.iters / a.shard / r1 / 1e3:.0f} / {W * H * a.iters / a.shard / r2 / 1e3:.0f} / "
-              f"{W * H * a.iters / a.shard / r3 / 1e3:.0f} Msamples/s)", flush=True)
-
+    n_paths = W * H * a.iters / a.shard
+    for rnd in range(a.rounds):
+        ts = [run(ctxs[:n], a.steps) for n in a.contexts]
+        print(f"round {rnd} grid {a.grid or 'full'} shard 1/{a.shard}: " +
+              ", ".join(f"{n} in flight {t:.3f} ms ({n_paths / t / 1e3:.0f} Msamples/s)" for n, t in zip(a.contexts, ts)),
+              flush=True)
 
 if __name__ == "__main__":
     main()
