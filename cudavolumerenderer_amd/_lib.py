@@ -28,6 +28,7 @@ SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4, "VdbSpa
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
+OPT_WORLD_TO_AABB, OPT_MK_COMPACTION = 18, 19
 
 
 class CvrError(RuntimeError):
@@ -75,6 +76,13 @@ PATH_RECORD_DTYPE = np.dtype([("image_id", "<u4"), ("flags", "<u4"), ("T", "<f4"
                               ("n_segments", "<u4"), ("n_steps", "<u4"), ("n_density", "<u4"),
                               ("n_albedo", "<u4")])
 assert PATH_RECORD_DTYPE.itemsize == C.sizeof(PathRecord)
+
+
+class LoadOptions(C.Structure):
+    _fields_ = [("flags", C.c_uint32), ("default_albedo", C.c_float * 3)]
+
+
+LOAD_DEFAULT_ALBEDO = 1
 
 
 class RenderDesc(C.Structure):
@@ -136,6 +144,7 @@ def load() -> C.CDLL:
         "cvr_tiling": (I32, [U32, U32, U32, U32, C.POINTER(U32)]),
         "cvr_tile_origin": (I32, [U32, U32, C.POINTER(U32), C.POINTER(U32)]),
         "cvr_scene_load": (I32, [C.c_char_p, I32, C.POINTER(P)]),
+        "cvr_scene_load_ex": (I32, [C.c_char_p, I32, C.POINTER(LoadOptions), C.POINTER(P)]),
         "cvr_scene_synthetic": (I32, [C.c_char_p, U32, C.POINTER(U32), C.POINTER(P)]),
         "cvr_scene_medium": (I32, [P, C.POINTER(MediumDesc)]),
         "cvr_scene_camera": (I32, [P, U32, U32, P, P]),
@@ -232,10 +241,19 @@ class Scene:
         return cls(h)
 
     @classmethod
-    def load(cls, path: str, scene_type: str = "Auto") -> "Scene":
+    def load(cls, path: str, scene_type: str = "Auto", default_albedo: Optional[Sequence[float]] = None) -> "Scene":
+        """Load a scene file (cvr_scene_load_ex).  default_albedo (r, g, b): a VDB
+        file without an albedo grid loads with that albedo everywhere (quirk
+        Q17's flag; the reference refuses such files, VDBAdapter.cpp:32-37)."""
         lib = load()
         h = C.c_void_p()
-        _check(lib.cvr_scene_load(path.encode(), SCENE_TYPES[scene_type], C.byref(h)))
+        opts = None
+        if default_albedo is not None:
+            opts = LoadOptions()
+            opts.flags = LOAD_DEFAULT_ALBEDO
+            opts.default_albedo[:] = [float(v) for v in default_albedo]
+        _check(lib.cvr_scene_load_ex(path.encode(), SCENE_TYPES[scene_type],
+                                     C.byref(opts) if opts is not None else None, C.byref(h)))
         return cls(h)
 
     def camera(self, width: int, height: int):

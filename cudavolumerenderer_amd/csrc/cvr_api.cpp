@@ -124,6 +124,8 @@ struct cvr_ctx {
   uint32_t grid_override = 0;
   int scatter_eps = -1;
   int rng_binding = 0;  // CVR_OPT_RNG_BINDING
+  int world_to_aabb = 0;  // CVR_OPT_WORLD_TO_AABB (Q4)
+  int mk_compaction = 0;  // CVR_OPT_MK_COMPACTION (Q11)
 
   int cu_count = 0;
   int persistent_grid = 0;
@@ -158,7 +160,11 @@ struct cvr_ctx {
 // d_work layout: 8 queue heads one 64-byte line apart, then 16 u64 stats
 // (single-kernel launches / wavefront events, wavefront track), then 8 u64
 // diagnostic counters (CVR_STAMPS builds).
-constexpr size_t kWorkQueues = 0, kWorkStats = 512, kWorkDebug = 640, kWorkBytes = 1024;
+#ifndef CVR_TAILSTAMPS
+#define CVR_TAILSTAMPS 0
+#endif
+constexpr size_t kWorkQueues = 0, kWorkStats = 512, kWorkDebug = 640,
+                 kWorkBytes = CVR_TAILSTAMPS ? 1024 + (size_t)80 * 65536 : 1024;
 
 #define HIP_TRY(ctx, expr)                                                                         \
   do {                                                                                                  \
@@ -215,9 +221,9 @@ int ensure_output(cvr_ctx* c) {
   const size_t px = (size_t)c->tile_w * c->tile_h;
   if (px == 0) return set_err(&c->err, CVR_ERR_STATE, "resolution not set");
   if (c->out_owned_px < px) {
+    // the old framebuffer may still be written by a launch in flight
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (c->d_out_owned) (void)hipFree(c->d_out_owned);
-  if (c->d_block_perm) (void)hipFree(c->d_block_perm);
-  if (c->d_zperm) (void)hipFree(c->d_zperm);
     c->d_out_owned = nullptr;
     HIP_TRY(c, hipMalloc(&c->d_out_owned, px * sizeof(float4)));
     HIP_TRY(c, hipMemsetAsync(c->d_out_owned, 0, px * sizeof(float4), c->stream));
@@ -309,6 +315,21 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   L.div_tile_w = make_fastdiv(L.tile_w);
   L.div_block = make_fastdiv(64u * L.samples);
   L.div_blocks_x = make_fastdiv(L.blocks_x);
+}
+
+// The medium as the kernels see it for this context's options: with the Q4
+// fix (CVR_OPT_WORLD_TO_AABB 1) the Woodcock coordinate is (p - min) scaled by
+// (res - 1)/extent instead of p - min/extent (cvr_walk.h MediumParams::gx).
+cvr::MediumParams launch_medium(const cvr_ctx* c) {
+  cvr::MediumParams m = c->m;
+  if (c->world_to_aabb) {
+    const float ex = m.bmax.x - m.bmin.x, ey = m.bmax.y - m.bmin.y, ez = m.bmax.z - m.bmin.z;
+    m.shift = m.bmin;
+    m.gx = m.agx / ex;
+    m.gy = m.agy / ey;
+    m.gz = m.agz / ez;
+  }
+  return m;
 }
 
 int check_ready(cvr_ctx* c) {
@@ -417,9 +438,9 @@ int wf_render(cvr_ctx* c, const cvr::LaunchParams& L, bool eps) {
     HIP_TRY(c, hipMemsetAsync(Pi.alive, 0, 4, s));
     const bool tm = c->wf_timing && timed_its < 512;
     if (tm) HIP_TRY(c, hipEventRecord(c->it_events[3 * timed_its], s));
-    HIP_TRY(c, cvr::wf_launch_events(c->m, L, Pi, eps, s));
+    HIP_TRY(c, cvr::wf_launch_events(launch_medium(c), L, Pi, eps, s));
     if (tm) HIP_TRY(c, hipEventRecord(c->it_events[3 * timed_its + 1], s));
-    HIP_TRY(c, cvr::wf_launch_track(c->m, L, Pi, (uint32_t)c->track_grid, s));
+    HIP_TRY(c, cvr::wf_launch_track(launch_medium(c), L, Pi, (uint32_t)c->track_grid, s));
     if (tm) {
       HIP_TRY(c, hipEventRecord(c->it_events[3 * timed_its + 2], s));
       ++timed_its;
@@ -447,6 +468,59 @@ int wf_render(cvr_ctx* c, const cvr::LaunchParams& L, bool eps) {
   c->last_iterations = it;
   c->last_track_ms = track_ms;
   c->last_events_ms = events_ms;
+  return CVR_OK;
+}
+
+// naiveMK with the reference's compaction count (quirk Q11 reproduced,
+// CVR_OPT_MK_COMPACTION 1): NaiveVolPTmk::launchRender / extend
+// (RenderKernelLauncher.cu:183-272).  Per iteration: d_init over the tile,
+// then bounces while the processed count is non-zero; after each bounce the
+// count is (live paths) - 1 and the live path with the highest pixel id (last
+// in the stable remove_if's output) is never extended again.  A bounce that
+// leaves no live path makes the reference's uint count wrap to 2^32 - 1 (its
+// next extend reads stale active-list entries, its remove_if runs off the
+// array): reported as CVR_ERR_STATE.  One host sync per bounce, as the
+// reference's thrust call.
+int mk_reference_render(cvr_ctx* c, const cvr::LaunchParams& L) {
+  if (L.path_first != 0 || L.tile_px == 0 || L.path_count % L.tile_px != 0 || c->shard_world != 1)
+    return set_err(&c->err, CVR_ERR_UNSUPPORTED,
+                   "naiveMK with the reference compaction renders whole tiles only (no path range / shard)");
+  const uint32_t iters = L.path_count / L.tile_px;
+  const cvr::MediumParams m = launch_medium(c);
+  float4* st = nullptr;
+  uint32_t* live = nullptr;
+  cvr::MkCtl* ctl = nullptr;
+  HIP_TRY(c, hipMalloc(&st, (size_t)L.tile_px * 3 * sizeof(float4)));
+  hipError_t e = hipMalloc(&live, (size_t)L.tile_px * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMalloc(&ctl, sizeof(cvr::MkCtl));
+  int r = CVR_OK;
+  for (uint32_t it = 0; it < iters && e == hipSuccess && r == CVR_OK; ++it) {
+    e = cvr::launch_mk_init(m, L, it, st, live, c->stream);
+    uint64_t n_processed = L.tile_px;
+    for (uint32_t depth = 0; n_processed != 0 && e == hipSuccess; ++depth) {
+      if (e == hipSuccess) e = hipMemsetAsync(ctl, 0, sizeof(cvr::MkCtl), c->stream);
+      if (e == hipSuccess) e = cvr::launch_mk_extend(m, L, it, depth, st, live, ctl, c->stream);
+      cvr::MkCtl h{};
+      if (e == hipSuccess) e = hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+      if (e != hipSuccess) break;
+      if (h.count == 0) {
+        r = set_err(&c->err, CVR_ERR_STATE,
+                    "naiveMK reference compaction (Q11): iteration %u bounce %u left no live path, so "
+                    "end - begin - 1 underflows (RenderKernelLauncher.cu:271)",
+                    it, depth);
+        break;
+      }
+      n_processed = h.count - 1u;
+      e = hipMemsetAsync(live + h.max_id, 0, sizeof(uint32_t), c->stream);  // dropped, never extended again
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(st);
+  if (live) (void)hipFree(live);
+  if (ctl) (void)hipFree(ctl);
+  if (r) return r;
+  if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "naiveMK reference compaction: %s", hipGetErrorString(e));
   return CVR_OK;
 }
 
@@ -516,6 +590,8 @@ int cvr_destroy(cvr_ctx* c) {
   if (c->d_out_owned) (void)hipFree(c->d_out_owned);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->d_pool_T) (void)hipFree(c->d_pool_T);
+  if (c->d_block_perm) (void)hipFree(c->d_block_perm);
+  if (c->d_zperm) (void)hipFree(c->d_zperm);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
   if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -552,9 +628,9 @@ static void fill_medium_common(cvr::MediumParams& m, const uint32_t res[3], cons
   m.fres_x = (float)res[0];
   m.fres_y = (float)res[1];
   m.fres_z = (float)res[2];
-  m.gx = (float)(res[0] - 1u);
-  m.gy = (float)(res[1] - 1u);
-  m.gz = (float)(res[2] - 1u);
+  m.gx = m.agx = (float)(res[0] - 1u);
+  m.gy = m.agy = (float)(res[1] - 1u);
+  m.gz = m.agz = (float)(res[2] - 1u);
   m.bmin = cvr::V3{box_min[0], box_min[1], box_min[2]};
   m.bmax = cvr::V3{box_max[0], box_max[1], box_max[2]};
   const float ex = box_max[0] - box_min[0], ey = box_max[1] - box_min[1], ez = box_max[2] - box_min[2];
@@ -1013,6 +1089,14 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "rng binding must be 0 (path) or 1 (thread)");
       c->rng_binding = (int)v;
       return CVR_OK;
+    case CVR_OPT_WORLD_TO_AABB:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "world_to_aabb must be 0 (reference) or 1 (fixed)");
+      c->world_to_aabb = (int)v;
+      return CVR_OK;
+    case CVR_OPT_MK_COMPACTION:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "mk_compaction must be 0 (fixed) or 1 (reference)");
+      c->mk_compaction = (int)v;
+      return CVR_OK;
     case CVR_OPT_SCATTER_EPS:
       if (v < -1 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "scatter_eps must be -1, 0 or 1");
       c->scatter_eps = (int)v;
@@ -1128,17 +1212,19 @@ int cvr_launch_render(cvr_ctx* c) {
       L.n_queues = 1;
     }
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 16u;
-    HIP_TRY(c, cvr::launch_regen_thread(c->m, L, eps, grid, c->stream));
+    HIP_TRY(c, cvr::launch_regen_thread(launch_medium(c), L, eps, grid, c->stream));
   } else if (c->kernel == CVR_KERNEL_NAIVE_SK) {
-    HIP_TRY(c, cvr::launch_naive(c->m, L, eps, c->stream));
+    HIP_TRY(c, cvr::launch_naive(launch_medium(c), L, eps, c->stream));
+  } else if (c->kernel == CVR_KERNEL_NAIVE_MK && c->mk_compaction) {
+    if ((r = mk_reference_render(c, L))) return r;
   } else if (c->kernel == CVR_KERNEL_NAIVE_MK) {
-    HIP_TRY(c, cvr::launch_naive_mk(c->m, L, c->stream));
+    HIP_TRY(c, cvr::launch_naive_mk(launch_medium(c), L, c->stream));
   } else if (scheduler_for(c) == 0) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
-    HIP_TRY(c, cvr::launch_persistent(c->m, L, eps, c->waves, grid, c->stream));
+    HIP_TRY(c, cvr::launch_persistent(launch_medium(c), L, eps, c->waves, grid, c->stream));
   } else if (scheduler_for(c) == 2) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->pool_grid;
-    HIP_TRY(c, cvr::launch_pool(c->m, L, eps, grid, c->stream));
+    HIP_TRY(c, cvr::launch_pool(launch_medium(c), L, eps, grid, c->stream));
   } else if (scheduler_for(c) == 3) {
     const bool sparse = c->m.leaves != nullptr;
     const int waves = wpool_waves_for(c, sparse);
@@ -1154,7 +1240,7 @@ int cvr_launch_render(cvr_ctx* c) {
     }
     L.pool_T = c->d_pool_T;
     L.rec = c->d_rec_active;
-    HIP_TRY(c, cvr::launch_wpool(c->m, L, eps, waves, grid, c->stream));
+    HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }
@@ -1244,6 +1330,16 @@ int cvr_debug_counters(cvr_ctx* c, uint64_t out[16]) {
   return CVR_OK;
 }
 
+#if CVR_TAILSTAMPS
+// Diagnostic build only: the wave pool's per-wave stamps (10 u64 per wave, cvr_wpool.hip).
+int cvr_debug_tailstamps(cvr_ctx* c, uint64_t* out, size_t n_waves) {
+  if (!c || !out || n_waves > 65536) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "bad argument");
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  HIP_TRY(c, hipMemcpy(out, c->d_work + kWorkStats + 64 * 8, n_waves * 80, hipMemcpyDeviceToHost));
+  return CVR_OK;
+}
+#endif
+
 int cvr_copy_output(cvr_ctx* c, float* host, float scale) {
   if (!c || !host) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
@@ -1309,7 +1405,7 @@ int cvr_trace_paths(cvr_ctx* c, uint32_t first, uint32_t count, cvr_path_record*
   fill_launch(c, L, first, count, /*sharded=*/false);
   cvr::PathRecord* d_rec = nullptr;
   HIP_TRY(c, hipMalloc(&d_rec, (size_t)count * sizeof(cvr::PathRecord)));
-  hipError_t e = cvr::launch_trace(c->m, L, scatter_eps_for(c), d_rec, c->stream);
+  hipError_t e = cvr::launch_trace(launch_medium(c), L, scatter_eps_for(c), d_rec, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess)
     e = hipMemcpy(out, d_rec, (size_t)count * sizeof(cvr::PathRecord), hipMemcpyDeviceToHost);

@@ -57,6 +57,17 @@ uint32_t wpool_slots(int waves, bool sparse);
 hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
                                hipStream_t s);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
+// naiveMK with the reference's compaction count (CVR_OPT_MK_COMPACTION 1):
+// d_init over the tile's pixels, then one d_extend launch per bounce; `st`
+// holds 3 float4 per pixel, `live` one flag, `ctl` the bounce's survivors.
+struct MkCtl {
+  uint32_t count;   // live paths after the bounce
+  uint32_t max_id;  // highest live pixel id (the one end - begin - 1 drops)
+};
+hipError_t launch_mk_init(const MediumParams& m, const LaunchParams& L, uint32_t iteration, float4* st,
+                          uint32_t* live, hipStream_t s);
+hipError_t launch_mk_extend(const MediumParams& m, const LaunchParams& L, uint32_t iteration, uint32_t depth,
+                            float4* st, uint32_t* live, MkCtl* ctl, hipStream_t s);
 hipError_t launch_image_to_host(const float* src, float* dst, size_t n, float scale, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);

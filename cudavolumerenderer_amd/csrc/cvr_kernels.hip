@@ -99,6 +99,79 @@ __global__ __launch_bounds__(256) void k_naive_mk(MediumParams m, LaunchParams L
   flush_stats(L, c);
 }
 
+// ------------------------------------------ naiveMK, reference compaction --
+// CVR_OPT_MK_COMPACTION 1 (quirk Q11 reproduced): the reference's per-bounce
+// kernel sequence over the tile's pixels (NaiveVolPTmk::launchRender / extend,
+// RenderKernelLauncher.cu:183-272).  Path state per pixel in `st` (o, d, T as
+// three float4) with a live flag; after each bounce the host reads the number
+// of live paths and the highest live pixel id (MkCtl), which the reference's
+// stable remove_if leaves last in its active list and its count
+// end - begin - 1 then drops.
+__global__ __launch_bounds__(256) void k_mk_init(MediumParams m, LaunchParams L, uint32_t iteration,
+                                                 float4* __restrict__ st, uint32_t* __restrict__ live) {
+  const uint32_t img = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (img < L.tile_px) {
+    PathState ps;
+    const uint32_t r = mk_init(m, L, iteration, img, ps);
+    c[STAT_PATHS] = 1;
+    c[STAT_SEGMENTS] = 1;
+    live[img] = r == MK_ALIVE ? 1u : 0u;
+    if (r == MK_MISSED) {  // d_output[img_id] += (1,1,1,1); w = 1 as every contribution here
+      splat(L, ps);
+      c[STAT_ESCAPED] = 1;
+    } else if (r == MK_ALIVE) {
+      st[3 * (size_t)img] = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
+      st[3 * (size_t)img + 1] = make_float4(ps.d.x, ps.d.y, ps.d.z, 0.0f);
+      st[3 * (size_t)img + 2] = make_float4(ps.T.x, ps.T.y, ps.T.z, 0.0f);
+    }
+  }
+  flush_stats(L, c);
+}
+
+__global__ __launch_bounds__(256) void k_mk_extend(MediumParams m, LaunchParams L, uint32_t iteration, uint32_t depth,
+                                                   float4* __restrict__ st, uint32_t* __restrict__ live,
+                                                   MkCtl* __restrict__ ctl) {
+  const uint32_t img = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  bool alive = false;
+  if (img < L.tile_px && live[img]) {
+    PathState ps;
+    ps.image_id = img;
+    const float4 a = st[3 * (size_t)img], b = st[3 * (size_t)img + 1], f = st[3 * (size_t)img + 2];
+    ps.o = mk3(a.x, a.y, a.z);
+    ps.d = mk3(b.x, b.y, b.z);
+    ps.T = mk3(f.x, f.y, f.z);
+    c[STAT_SEGMENTS] = 1;
+    const uint32_t r =
+        mk_extend(m, iteration, depth, ps, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH], c[STAT_ALBEDO]);
+    if (r == MK_ESCAPED) {
+      splat(L, ps);
+      c[STAT_ESCAPED] = 1;
+    }
+    if (r == MK_ALIVE) {
+      st[3 * (size_t)img] = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
+      st[3 * (size_t)img + 1] = make_float4(ps.d.x, ps.d.y, ps.d.z, 0.0f);
+      st[3 * (size_t)img + 2] = make_float4(ps.T.x, ps.T.y, ps.T.z, 0.0f);
+      alive = true;
+    } else {
+      live[img] = 0u;
+    }
+  }
+  // wave-aggregated survivors: count and highest pixel id
+  const unsigned long long mask = __ballot(alive);
+  if (mask) {
+    uint32_t mx = alive ? img : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+    if ((threadIdx.x & 63u) == 0u) {
+      atomicAdd(&ctl->count, (uint32_t)__popcll(mask));
+      atomicMax(&ctl->max_id, mx);
+    }
+  }
+  flush_stats(L, c);
+}
+
 // --------------------------------------------------------------- trace ----
 template <bool kScatterEps>
 __global__ __launch_bounds__(256) void k_trace(MediumParams m, LaunchParams L, PathRecord* rec) {
@@ -422,6 +495,19 @@ hipError_t launch_naive(const MediumParams& m, const LaunchParams& L, bool scatt
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s) {
   if (L.path_count == 0) return hipSuccess;
   hipLaunchKernelGGL(k_naive_mk, dim3((L.path_count + 255u) / 256u), dim3(256), 0, s, m, L);
+  return hipGetLastError();
+}
+
+hipError_t launch_mk_init(const MediumParams& m, const LaunchParams& L, uint32_t iteration, float4* st,
+                          uint32_t* live, hipStream_t s) {
+  hipLaunchKernelGGL(k_mk_init, dim3((L.tile_px + 255u) / 256u), dim3(256), 0, s, m, L, iteration, st, live);
+  return hipGetLastError();
+}
+
+hipError_t launch_mk_extend(const MediumParams& m, const LaunchParams& L, uint32_t iteration, uint32_t depth,
+                            float4* st, uint32_t* live, MkCtl* ctl, hipStream_t s) {
+  hipLaunchKernelGGL(k_mk_extend, dim3((L.tile_px + 255u) / 256u), dim3(256), 0, s, m, L, iteration, depth, st, live,
+                     ctl);
   return hipGetLastError();
 }
 

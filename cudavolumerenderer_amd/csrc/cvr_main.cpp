@@ -27,7 +27,8 @@ namespace {
 
 struct Options {
   std::string scene_file, scene_type = "Auto", algorithm = "cudaVolPath", kernel = "regenerationSK";
-  std::string output, synthetic, rng_binding = "path";
+  std::string output, synthetic, rng_binding = "path", world_to_aabb = "reference", mk_compaction = "fixed";
+  std::vector<float> default_albedo;
   bool interactive = true, unified = false;
   unsigned trials = 1, iterations = 20, device = 0, seed = 0;
   std::vector<unsigned> tiles{1, 1}, resolution{1024, 1024};
@@ -55,7 +56,13 @@ void usage() {
       "  --synthetic bucky|manix|hetvol|cloud  use a built-in proxy scene\n"
       "  --device N, --seed S\n"
       "  --rng-binding path|thread (=path)  regenerationSK: thread = the reference's Rng(seed + tid)\n"
-      "                                     per persistent thread (non-deterministic, SURVEY Q2)\n");
+      "                                     per persistent thread (non-deterministic, SURVEY Q2)\n"
+      "  --default-albedo r g b             VDB files without an albedo grid load with this albedo\n"
+      "                                     (the reference refuses them, SURVEY Q17)\n"
+      "  --world-to-aabb reference|fixed (=reference)  Woodcock density coordinate: the reference's\n"
+      "                                     p - min/extent, or (p - min)/extent (SURVEY Q4)\n"
+      "  --mk-compaction fixed|reference (=fixed)  naiveMK: keep every live path, or the reference's\n"
+      "                                     end - begin - 1 (drops one per bounce, SURVEY Q11)\n");
 }
 
 bool is_flag(const char* a) { return a[0] == '-' && !(a[1] >= '0' && a[1] <= '9'); }
@@ -94,6 +101,18 @@ int parse(int argc, char** argv, Options& o) {
     else if (a == "--device") o.device = (unsigned)strtoul(need("device").c_str(), nullptr, 10);
     else if (a == "--rng-binding") o.rng_binding = need("rng-binding");
     else if (a == "--seed") o.seed = (unsigned)strtoul(need("seed").c_str(), nullptr, 10);
+    else if (a == "--world-to-aabb") o.world_to_aabb = need("world-to-aabb");
+    else if (a == "--mk-compaction") o.mk_compaction = need("mk-compaction");
+    else if (a == "--default-albedo") {
+      o.default_albedo.clear();
+      while (i + 1 < argc && o.default_albedo.size() < 3 && !(argv[i + 1][0] == '-' && argv[i + 1][1] == '-'))
+        o.default_albedo.push_back(strtof(argv[++i], nullptr));
+      if (o.default_albedo.size() == 1) o.default_albedo.resize(3, o.default_albedo[0]);
+      if (o.default_albedo.size() != 3) {
+        fprintf(stderr, "[ConfigParser] Error: --default-albedo needs 1 or 3 values\n");
+        return 2;
+      }
+    }
     else if (!is_flag(a.c_str()) && o.scene_file.empty()) o.scene_file = a;  // positional
     else {
       fprintf(stderr, "[ConfigParser] Error: unrecognised option '%s'\n", a.c_str());
@@ -148,7 +167,12 @@ int main(int argc, char** argv) {
       fprintf(stderr, "Error: scene type not correct\n");
       return 2;
     }
-    r = cvr_scene_load(o.scene_file.c_str(), st, &scene);
+    cvr_load_options lo{};
+    if (!o.default_albedo.empty()) {
+      lo.flags = CVR_LOAD_DEFAULT_ALBEDO;
+      for (int k = 0; k < 3; ++k) lo.default_albedo[k] = o.default_albedo[k];
+    }
+    r = cvr_scene_load_ex(o.scene_file.c_str(), st, &lo, &scene);
   }
   if (r != CVR_OK) {
     fprintf(stderr, "Error: could not load scene (%d): %s\n", r, cvr_last_error(nullptr));
@@ -191,6 +215,19 @@ int main(int argc, char** argv) {
       return 2;
     }
     if (o.rng_binding == "thread" && (r = cvr_set_option(ctx, CVR_OPT_RNG_BINDING, 1)) != CVR_OK) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
+      return 1;
+    }
+    if (o.world_to_aabb != "reference" && o.world_to_aabb != "fixed") {
+      fprintf(stderr, "[ConfigParser] Error: --world-to-aabb must be reference or fixed\n");
+      return 2;
+    }
+    if (o.mk_compaction != "fixed" && o.mk_compaction != "reference") {
+      fprintf(stderr, "[ConfigParser] Error: --mk-compaction must be fixed or reference\n");
+      return 2;
+    }
+    if ((o.world_to_aabb == "fixed" && (r = cvr_set_option(ctx, CVR_OPT_WORLD_TO_AABB, 1)) != CVR_OK) ||
+        (o.mk_compaction == "reference" && (r = cvr_set_option(ctx, CVR_OPT_MK_COMPACTION, 1)) != CVR_OK)) {
       fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
       return 1;
     }

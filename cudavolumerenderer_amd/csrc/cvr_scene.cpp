@@ -435,7 +435,16 @@ int cvr_scene_synthetic(const char* name, uint32_t seed, const uint32_t* dims, c
 }
 
 int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
+  return cvr_scene_load_ex(path, scene_type, nullptr, out);
+}
+
+int cvr_scene_load_ex(const char* path, int scene_type, const cvr_load_options* opts, cvr_scene** out) {
   if (!path || !out) return CVR_ERR_INVALID;
+  if (opts && (opts->flags & ~(uint32_t)CVR_LOAD_DEFAULT_ALBEDO)) {
+    set_last_error("unknown load option flags");
+    return CVR_ERR_INVALID;
+  }
+  const float* default_albedo = (opts && (opts->flags & CVR_LOAD_DEFAULT_ALBEDO)) ? opts->default_albedo : nullptr;
   *out = nullptr;
   std::string p(path);
   int type = scene_type;
@@ -462,7 +471,7 @@ int cvr_scene_load(const char* path, int scene_type, cvr_scene** out) {
       r = (got == raw.size()) ? scene_from_raw_bytes(raw, p, s) : CVR_ERR_IO;  // Q16: report short files
     }
   } else if (type == CVR_SCENE_VDB || type == CVR_SCENE_VDB_SPARSE) {
-    r = load_vdb_scene(p, s, type == CVR_SCENE_VDB_SPARSE);
+    r = load_vdb_scene(p, s, type == CVR_SCENE_VDB_SPARSE, default_albedo);
   } else if (type == CVR_SCENE_MHD) {
     r = load_mhd_scene(p, s);
   } else if (type == CVR_SCENE_MITSUBA_XML) {

@@ -32,7 +32,7 @@ struct cvr_scene {
 namespace cvr {
 int scene_from_raw_bytes(const std::vector<uint8_t>& raw, const std::string& name, cvr_scene* s);
 void finish_vdb_like(cvr_scene* s);
-int load_vdb_scene(const std::string& path, cvr_scene* s, bool sparse);
+int load_vdb_scene(const std::string& path, cvr_scene* s, bool sparse, const float* default_albedo);
 int load_mhd_scene(const std::string& path, cvr_scene* s);
 int load_xml_scene(const std::string& path, cvr_scene* s);
 void camera_for_fov(float fov_x, uint32_t w, uint32_t h, float inv_view[12], float r2v[2]);

@@ -424,9 +424,12 @@ int read_grid(const std::vector<uint8_t>& file, const GridDesc& gd, Tree<VS>& tr
 // what densification leaves there.  The albedo must share the density box
 // (converter-made files do), so the reference's reinterpretation of the
 // albedo array with the density's dimensions is the identity.
+// Without an albedo tree (a density-only file read with a default albedo,
+// quirk Q17's flag) the leaves carry no albedo and the background is
+// `default_albedo` everywhere.
 template <int VD, int VA>
-int vdb_to_leaves(const Tree<VD>& dt, const Tree<VA>& at, const int32_t lo[3], const uint32_t dim[3],
-                  cvr_scene* sc) {
+int vdb_to_leaves(const Tree<VD>& dt, const Tree<VA>* at, const int32_t lo[3], const uint32_t dim[3],
+                  const float* default_albedo, cvr_scene* sc) {
   const uint32_t lnx = (dim[0] + 7) / 8, lny = (dim[1] + 7) / 8, lnz = (dim[2] + 7) / 8;
   const size_t nleaf = (size_t)lnx * lny * lnz;
   if (nleaf > (1ull << 30)) return fail("density bounding box too large for the leaf table");
@@ -455,7 +458,7 @@ int vdb_to_leaves(const Tree<VD>& dt, const Tree<VA>& at, const int32_t lo[3], c
     if (f != 0.0f) sc->leaf_density[slot_of(x - lo[0], y - lo[1], z - lo[2])] = f;
   });
   bool albedo_set = false;
-  at.for_each_on([&](int32_t x, int32_t y, int32_t z, const uint8_t* v) {
+  if (at) at->for_each_on([&](int32_t x, int32_t y, int32_t z, const uint8_t* v) {
     float c[3];
     memcpy(c, v, 12);
     if (c[0] == 0.0f && c[1] == 0.0f && c[2] == 0.0f) return;
@@ -466,7 +469,8 @@ int vdb_to_leaves(const Tree<VD>& dt, const Tree<VA>& at, const int32_t lo[3], c
     albedo_set = true;
   });
   if (!albedo_set) std::vector<float>().swap(sc->leaf_albedo);
-  const float bg[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  float bg[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  if (!at && default_albedo) memcpy(bg, default_albedo, 3 * sizeof(float));
   memcpy(sc->albedo_bg, bg, sizeof(bg));
   sc->sparse_only = true;
   sc->have_leaves = true;
@@ -479,7 +483,7 @@ int vdb_to_leaves(const Tree<VD>& dt, const Tree<VA>& at, const int32_t lo[3], c
   return CVR_OK;
 }
 
-int load_vdb_scene(const std::string& path, cvr_scene* sc, bool sparse) {
+int load_vdb_scene(const std::string& path, cvr_scene* sc, bool sparse, const float* default_albedo) {
   FILE* fp = fopen(path.c_str(), "rb");
   if (!fp) return fail("cannot open " + path);
   std::vector<uint8_t> file;
@@ -516,18 +520,23 @@ int load_vdb_scene(const std::string& path, cvr_scene* sc, bool sparse) {
     if (!grids.count(gd.name)) grids[gd.name] = gd;
   }
   if (!s.ok) return fail("grid descriptors");
-  // VDBAdapter::loadVDBFile: both grids are required (quirk Q17)
+  // VDBAdapter::loadVDBFile (VDBAdapter.cpp:32-37): both grids are required
+  // (quirk Q17), unless the caller gives a default albedo for files without one
   if (!grids.count("density")) return fail("VDB file does not contain a density grid");
-  if (!grids.count("albedo")) return fail("VDB file does not contain an albedo grid");
+  const bool has_albedo = grids.count("albedo") != 0;
+  if (!has_albedo && !default_albedo)
+    return fail("VDB file does not contain an albedo grid (give a default albedo: --default-albedo r g b)");
   const GridDesc& gd = grids["density"];
-  const GridDesc& ga = grids["albedo"];
   if (gd.type != "Tree_float_5_4_3") return fail("density grid type " + gd.type + " is not supported");
-  if (ga.type != "Tree_vec3s_5_4_3") return fail("albedo grid type " + ga.type + " is not supported");
   Tree<4> dt;
   Tree<12> at;
   int r = read_grid(file, gd, dt);
   if (r) return r;
-  if ((r = read_grid(file, ga, at))) return r;
+  if (has_albedo) {
+    const GridDesc& ga = grids["albedo"];
+    if (ga.type != "Tree_vec3s_5_4_3") return fail("albedo grid type " + ga.type + " is not supported");
+    if ((r = read_grid(file, ga, at))) return r;
+  }
   int32_t lo[3], hi[3], alo[3], ahi[3];
   if (!dt.bbox(lo, hi)) return fail("density grid has no active voxels");
   uint32_t dim[3], adim[3] = {0, 0, 0};
@@ -537,14 +546,23 @@ int load_vdb_scene(const std::string& path, cvr_scene* sc, bool sparse) {
   for (int k = 0; k < 3; ++k) sc->dims[k] = dim[k];
   // more than 2^30 voxels (20 GB of dense host arrays): read sparse
   if (sparse || n > (1ull << 30)) {
-    if (at.bbox(alo, ahi))
+    if (has_albedo && at.bbox(alo, ahi))
       for (int k = 0; k < 3; ++k)
         if (alo[k] != lo[k] || ahi[k] != hi[k])
           return fail("sparse VDB read needs the albedo grid on the density grid's bounding box");
-    return vdb_to_leaves(dt, at, lo, dim, sc);
+    return vdb_to_leaves(dt, has_albedo ? &at : nullptr, lo, dim, default_albedo, sc);
   }
   sc->density.assign(n, 0.0f);  // inactive value 0
   dt.densify(lo, dim, sc->density.data(), 1);
+  if (!has_albedo) {  // Q17 flag: the default albedo everywhere
+    sc->albedo.resize(n * 4);
+    for (size_t i = 0; i < n; ++i) {
+      memcpy(&sc->albedo[4 * i], default_albedo, 3 * sizeof(float));
+      sc->albedo[4 * i + 3] = 1.0f;
+    }
+    finish_vdb_like(sc);
+    return CVR_OK;
+  }
   // Albedo: densified over the albedo grid's own bounding box, then read as
   // if it had the density grid's dimensions (VDBSceneBuilder.h:57-66 indexes
   // it with volume_size_); identical boxes in every converter-made file.

@@ -133,9 +133,15 @@ struct MediumParams {
   uint32_t rx, ry, rz;
   uint32_t rxy;                  // rx * ry (< 2^24 for a dense medium)
   float fres_x, fres_y, fres_z;  // (float)res
-  float gx, gy, gz;  // (float)(res-1): DeviceVolume::volumeToGrid
+  // Woodcock density coordinate -> grid: cx = (p - shift) * gx.  Default
+  // (quirk Q4 reproduced): shift = box_min / extent (worldToAABB's operator
+  // precedence, Utilities.cuh:129-132) and gx = res - 1 (volumeToGrid).
+  // CVR_OPT_WORLD_TO_AABB 1: shift = box_min, gx = (res - 1) / extent, the
+  // intended (p - min)/extent folded into the grid scale (no extra step code).
+  float gx, gy, gz;
+  float agx, agy, agz;  // (float)(res-1): the albedo lookup's volumeToGrid (AABB::transform coordinates)
   V3 bmin, bmax;
-  V3 shift;          // box_min / extent  (worldToAABB precedence, Q4)
+  V3 shift;
   float scale;
   float inv_sigma;   // 1 / (scale * max_density)
   float g;           // HG asymmetry (0 in the reference, Q7)
@@ -259,8 +265,8 @@ struct Tri {
   uint32_t xa, xb, ya, yb, za, zb;
   float fx, fy, fz;
 };
-CVR_DEV Tri tri_setup(const MediumParams& m, V3 p) {
-  const float cx = p.x * m.gx, cy = p.y * m.gy, cz = p.z * m.gz;
+CVR_DEV Tri tri_setup(const MediumParams& m, V3 p, float gx, float gy, float gz) {
+  const float cx = p.x * gx, cy = p.y * gy, cz = p.z * gz;
   const int x1 = det_floor_i32(cx), y1 = det_floor_i32(cy), z1 = det_floor_i32(cz);
   Tri t;
   t.fx = cx - (float)x1;
@@ -320,7 +326,7 @@ CVR_DEV float4 texel_albedo(const MediumParams& m, uint32_t x, uint32_t y, uint3
 // The reference's 8-tap trilinear (Volume.h:47-69), used where no cell
 // applies (the Q5 wrap, points outside the grid).
 CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p) {
-  const Tri t = tri_setup(m, p);
+  const Tri t = tri_setup(m, p, m.gx, m.gy, m.gz);
   const float d000 = texel_density(m, t.xa, t.ya, t.za), d001 = texel_density(m, t.xb, t.ya, t.za);
   const float d010 = texel_density(m, t.xa, t.yb, t.za), d011 = texel_density(m, t.xb, t.yb, t.za);
   const float d100 = texel_density(m, t.xa, t.ya, t.zb), d101 = texel_density(m, t.xb, t.ya, t.zb);
@@ -331,7 +337,7 @@ CVR_DEV float density_lookup_gather(const MediumParams& m, V3 p) {
   return lerpf(a, b, t.fz, _fz);
 }
 CVR_DEV V3 albedo_lookup(const MediumParams& m, V3 p) {
-  const Tri t = tri_setup(m, p);
+  const Tri t = tri_setup(m, p, m.agx, m.agy, m.agz);
   const float _fx = 1.0f - t.fx, _fy = 1.0f - t.fy, _fz = 1.0f - t.fz;
   // one z plane at a time (same operations as the 8-tap form: x, then y
   // lerps per plane, then z), so at most 4 texels are live
@@ -782,24 +788,15 @@ CVR_DEV void rng_seeded(Rng& s, uint32_t iteration, uint32_t index, uint32_t dep
   rng_init(s, (int32_t)(utilhash(0x80000000u | (depth << 22) | iteration) ^ utilhash(index)));
 }
 
-// Outcome of one naiveMK path (flags as PathRecord: bit0 contributed T,
-// bit1 truncated, bit2 missed the box at init (T = 1), bit3 dropped by a
-// failed GGX sample at init).
-struct MkResult {
-  uint32_t flags;
-  V3 T;
-  uint32_t n_segments, n_steps, n_density, n_fetch, n_albedo;
-};
-
-// NaiveVolPTmk_kernel::d_init + the d_extend bounce loop (NaiveVolPTmk_kernel.cuh:20-151,
-// RenderKernelLauncher.cu:183-272) for path id = iteration * tile_px + pixel.
-// Per path the multi-kernel wavefront reduces to this loop: every live path
-// is extended once per launch, and compaction keeps every live path (quirk
-// Q11 fixed).  Same operation order as the oracle's trace_path_mk.
-CVR_DEV MkResult walk_mk(const MediumParams& m, const LaunchParams& L, uint32_t path_id) {
-  MkResult r{0u, mk3(1.0f, 1.0f, 1.0f), 1u, 0u, 0u, 0u, 0u};
-  const uint32_t image_id = path_id % L.tile_px, iteration = path_id / L.tile_px;
-  PathState ps;
+// NaiveVolPTmk_kernel::d_init (NaiveVolPTmk_kernel.cuh:20-77) for path id
+// = iteration * tile_px + image_id: camera ray on the (iteration, pixel, 0)
+// stream, AABB test, then the GGX sample at the box before any medium test
+// (Q12).  Returns MK_ALIVE (ps holds the path for the first d_extend),
+// MK_MISSED (the box was missed: the pixel gets (1,1,1)) or MK_DROPPED (a
+// failed GGX sample: no contribution).
+enum : uint32_t { MK_ALIVE = 0, MK_MISSED = 1, MK_DROPPED = 2, MK_ESCAPED = 3, MK_DIED = 4, MK_TRUNCATED = 5 };
+CVR_DEV uint32_t mk_init(const MediumParams& m, const LaunchParams& L, uint32_t iteration, uint32_t image_id,
+                         PathState& ps) {
   ps.image_id = image_id;
   rng_seeded(ps.rng, iteration, image_id, 0u);
   {
@@ -824,24 +821,80 @@ CVR_DEV MkResult walk_mk(const MediumParams& m, const LaunchParams& L, uint32_t 
   is.dist = 0.0f;
   is.normal = mk3(0, 0, 0);
   is.inside = false;
-  if (!aabb_intersect(m, ps.o, ps.d, is)) {
+  if (!aabb_intersect(m, ps.o, ps.d, is)) return MK_MISSED;
+  if (is.dist < 0.0f) is.dist = 0.0f;  // clamp to near plane
+  ps.o = add3(ps.o, scl3(ps.d, is.dist));
+  const Frame fr = frame_from_z(is.normal);
+  const V3 dir = frame_to_local(fr, normalize3(neg3(ps.d)));
+  float weight = 1.0f;
+  if (!ggx_sample(m, dir, ps.rng, ps.d, weight)) return MK_DROPPED;
+  ps.T = scl3(ps.T, weight);
+  ps.d = frame_to_world(fr, ps.d);
+  ps.o = add3(ps.o, scl3(ps.d, CVR_EPSILON_F));
+  return MK_ALIVE;
+}
+
+// One NaiveVolPTmk_kernel::d_extend bounce (NaiveVolPTmk_kernel.cuh:79-151)
+// of a live path at `depth`: re-seed from (iteration, pixel, depth), three
+// unused draws (Q12), one naiveSK segment (scatter with -eps), roulette.
+// Returns MK_ALIVE, MK_ESCAPED (splat ps.T) or MK_DIED (roulette).
+CVR_DEV uint32_t mk_extend(const MediumParams& m, uint32_t iteration, uint32_t depth, PathState& ps,
+                           uint32_t& n_steps, uint32_t& n_density, uint32_t& n_fetch, uint32_t& n_albedo) {
+  rng_seeded(ps.rng, iteration, ps.image_id, depth);
+  (void)rng_float(ps.rng);  // float3 e = rng.getFloat3(), unused (Q12)
+  (void)rng_float(ps.rng);
+  (void)rng_float(ps.rng);
+  Isect is;
+  is.dist = 0.0f;  // a fresh SimpleIsect per d_extend
+  is.normal = mk3(0, 0, 0);
+  is.inside = false;
+  if (!aabb_intersect(m, ps.o, ps.d, is)) return MK_ESCAPED;
+  float t = 0.0f;
+  bool collided = false;
+  if (is.inside) {
+    int s;
+    do {
+      s = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, n_steps, n_density, n_fetch);
+    } while (s == 0);
+    collided = t < is.dist;
+  }
+  if (!collided) {
+    boundary_event(m, ps, is);
+  } else {
+    scatter_event<true>(m, ps, t);
+    ++n_albedo;
+  }
+  return roulette(ps) ? MK_ALIVE : MK_DIED;
+}
+
+// Outcome of one naiveMK path (flags as PathRecord: bit0 contributed T,
+// bit1 truncated, bit2 missed the box at init (T = 1), bit3 dropped by a
+// failed GGX sample at init).
+struct MkResult {
+  uint32_t flags;
+  V3 T;
+  uint32_t n_segments, n_steps, n_density, n_fetch, n_albedo;
+};
+
+// NaiveVolPTmk_kernel::d_init + the d_extend bounce loop (NaiveVolPTmk_kernel.cuh:20-151,
+// RenderKernelLauncher.cu:183-272) for path id = iteration * tile_px + pixel.
+// Per path the multi-kernel wavefront reduces to this loop: every live path
+// is extended once per launch, and compaction keeps every live path (quirk
+// Q11 fixed; CVR_OPT_MK_COMPACTION 1 runs the reference's per-bounce launches,
+// k_mk_extend).  Same operation order as the oracle's trace_path_mk.
+CVR_DEV MkResult walk_mk(const MediumParams& m, const LaunchParams& L, uint32_t path_id) {
+  MkResult r{0u, mk3(1.0f, 1.0f, 1.0f), 1u, 0u, 0u, 0u, 0u};
+  const uint32_t image_id = path_id % L.tile_px, iteration = path_id / L.tile_px;
+  PathState ps;
+  const uint32_t s0 = mk_init(m, L, iteration, image_id, ps);
+  if (s0 == MK_MISSED) {
     r.flags = 1u | 4u;
     return r;
   }
-  if (is.dist < 0.0f) is.dist = 0.0f;  // clamp to near plane
-  ps.o = add3(ps.o, scl3(ps.d, is.dist));
-  {
-    const Frame fr = frame_from_z(is.normal);
-    const V3 dir = frame_to_local(fr, normalize3(neg3(ps.d)));
-    float weight = 1.0f;
-    if (!ggx_sample(m, dir, ps.rng, ps.d, weight)) {
-      r.flags = 8u;  // dropped: no contribution, T recorded as 0 (as the oracle)
-      r.T = mk3(0.0f, 0.0f, 0.0f);
-      return r;
-    }
-    ps.T = scl3(ps.T, weight);
-    ps.d = frame_to_world(fr, ps.d);
-    ps.o = add3(ps.o, scl3(ps.d, CVR_EPSILON_F));
+  if (s0 == MK_DROPPED) {
+    r.flags = 8u;  // dropped: no contribution, T recorded as 0 (as the oracle)
+    r.T = mk3(0.0f, 0.0f, 0.0f);
+    return r;
   }
   for (uint32_t depth = 0;; ++depth) {
     if (L.max_segments && r.n_segments >= L.max_segments) {
@@ -849,33 +902,9 @@ CVR_DEV MkResult walk_mk(const MediumParams& m, const LaunchParams& L, uint32_t 
       break;
     }
     ++r.n_segments;
-    rng_seeded(ps.rng, iteration, image_id, depth);
-    (void)rng_float(ps.rng);  // float3 e = rng.getFloat3(), unused (Q12)
-    (void)rng_float(ps.rng);
-    (void)rng_float(ps.rng);
-    is.dist = 0.0f;  // a fresh SimpleIsect per d_extend
-    is.normal = mk3(0, 0, 0);
-    is.inside = false;
-    if (!aabb_intersect(m, ps.o, ps.d, is)) {
-      r.flags |= 1u;
-      break;
-    }
-    float t = 0.0f;
-    bool collided = false;
-    if (is.inside) {
-      int s;
-      do {
-        s = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, r.n_steps, r.n_density, r.n_fetch);
-      } while (s == 0);
-      collided = t < is.dist;
-    }
-    if (!collided) {
-      boundary_event(m, ps, is);
-    } else {
-      scatter_event<true>(m, ps, t);
-      ++r.n_albedo;
-    }
-    if (!roulette(ps)) break;
+    const uint32_t e = mk_extend(m, iteration, depth, ps, r.n_steps, r.n_density, r.n_fetch, r.n_albedo);
+    if (e == MK_ESCAPED) r.flags |= 1u;
+    if (e != MK_ALIVE) break;
   }
   r.T = ps.T;
   return r;

@@ -31,6 +31,11 @@
 #ifndef CVR_STAMPS
 #define CVR_STAMPS 0
 #endif
+// Diagnostic build (tools/tailstamps.py): per-wave wall-clock stamps of the
+// launch's ramp-up and drain, written after the stats words.
+#ifndef CVR_TAILSTAMPS
+#define CVR_TAILSTAMPS 0
+#endif
 // Woodcock steps per track iteration between swap/event checks.
 #ifndef CVR_WPOOL_UNROLL
 #define CVR_WPOOL_UNROLL 4
@@ -216,6 +221,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   }
   static_assert(sizeof(WavePool<kSlots, kSplit>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves, kSplit>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
+  static_assert(kSlots <= 256, "the pool's rings and stacks hold slot indices as uint8_t");
   __shared__ WavePool<kSlots, kSplit> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
@@ -252,6 +258,13 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
 #if CVR_STAMPS
   unsigned long long t_regen = 0;
+#endif
+#if CVR_TAILSTAMPS
+  // start, first track iteration, queues exhausted, end (s_memrealtime, 100 MHz); track iterations,
+  // event batches (total, after exhaustion); lane-steps after exhaustion
+  const unsigned long long ts_start = __builtin_amdgcn_s_memrealtime();
+  unsigned long long ts_track = 0, ts_ex = 0, ts_n_tr = 0, ts_n_ev = 0, ts_n_tr_ex = 0, ts_n_ev_ex = 0;
+  uint32_t ts_steps_ex = 0;
 #endif
   for (;;) {
     // ================================================= TRACK ==============
@@ -317,6 +330,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
       ++st[3];
 #endif
+#if CVR_TAILSTAMPS
+      if (ts_track == 0) ts_track = __builtin_amdgcn_s_memrealtime();
+      ++ts_n_tr;
+      if (cur.exhausted) ++ts_n_tr_ex;
+#endif
 #pragma unroll
       for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
         // woodcock_step_core with both draws taken up front: a step that
@@ -356,6 +374,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
     // ================================================= EVENT ==============
     __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
+#if CVR_TAILSTAMPS
+    ++ts_n_ev;
+    if (cur.exhausted) ++ts_n_ev_ex;
+#endif
     // Event-code view of the medium: its BSDF / box / albedo fields pass
     // through opaque_s per batch, so values derived from them (HG and box
     // constants) are recomputed in the batch instead of being hoisted to the
@@ -466,6 +488,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             qsel = __shfl(qsel, 0);
             if (b == 0xFFFFFFFFu) {
               cur.exhausted = true;
+#if CVR_TAILSTAMPS
+              ts_ex = __builtin_amdgcn_s_memrealtime();
+              ts_steps_ex = c_steps;
+#endif
               break;
             }
             cur.q = cur.home = qsel;
@@ -607,6 +633,17 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
                                               S.cnt[STAT_ALBEDO], S.cnt[STAT_ESCAPED], S.cnt[STAT_TRUNCATED], fetch};
     if (lane < (uint32_t)STAT_COUNT && w[lane]) atomicAdd(L.stats + lane, w[lane]);
   }
+#if CVR_TAILSTAMPS
+  {
+    unsigned long long sx = c_steps - ts_steps_ex;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sx += __shfl_xor(sx, off);
+    const unsigned long long ts_end = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long hw = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
+    const unsigned long long v[10] = {ts_start, ts_track, ts_ex, ts_end, ts_n_tr, ts_n_ev, ts_n_tr_ex, ts_n_ev_ex, sx, hw};
+    if (lane < 10u) L.stats[64 + (size_t)blockIdx.x * 10 + lane] = v[lane];
+  }
+#endif
 #if CVR_STAMPS
   {
     const unsigned long long now = __builtin_amdgcn_s_memtime();

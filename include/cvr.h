@@ -90,10 +90,21 @@ typedef enum {
                                  (RegenerationVolPTsk_kernel.cuh:146-232).  Thread-bound results
                                  depend on which thread takes which path: deterministic only for a
                                  one-wave launch (CVR_OPT_GRID 1). */
-  CVR_OPT_MORTON = 17          /* pool scheduler (streamingSK): 1 sorts each track phase's paths by the
+  CVR_OPT_MORTON = 17,         /* pool scheduler (streamingSK): 1 sorts each track phase's paths by the
                                  Morton code of their origin in the box (MortonSort.h:28-49,
                                  StreamingVolPTsk_kernel.cuh:188-216); default 0 (measured slower
                                  here).  Scheduling only: results are unchanged. */
+  CVR_OPT_WORLD_TO_AABB = 18,  /* quirk Q4: 0 (default) the reference's worldToAABB, p - min/extent
+                                 (operator precedence, Utilities.cuh:129-132); 1 the intended
+                                 (p - min)/extent, computed as fma(p, 1/extent, -min/extent).  The two
+                                 agree for the unit box of VDB/Raw/MHD scenes. */
+  CVR_OPT_MK_COMPACTION = 19   /* quirk Q11, naiveMK only: 0 (default) every live path is extended
+                                 until it ends; 1 the reference's compaction count end - begin - 1
+                                 (RenderKernelLauncher.cu:266-271): after every bounce the live path
+                                 with the highest pixel id is dropped, and a bounce that leaves no live
+                                 path (the count underflows to 2^32 - 1 in the reference) fails the
+                                 launch with CVR_ERR_STATE.  Runs the reference's per-bounce kernel
+                                 sequence (one launch and host sync per bounce). */
 } cvr_option;
 
 /* HeterogeneousMedium + GGX boundary (Medium.h:110-190, Bsdf.h:17-30). */
@@ -299,6 +310,18 @@ int cvr_tile_origin(uint32_t tile_id, uint32_t ntx, const uint32_t tile_dim[2], 
  * (convert-mhd semantics), MitsubaXml.  AUTO picks by extension
  * (ConfigParser.cpp:79-97). */
 int cvr_scene_load(const char* path, int scene_type, cvr_scene** out);
+/* Extension: cvr_scene_load with options.  CVR_LOAD_DEFAULT_ALBEDO (quirk
+ * Q17's flag): a VDB file without an "albedo" grid, which the reference
+ * refuses (VDBAdapter.cpp:32-37), loads with albedo (r,g,b) everywhere, as
+ * the dense grid or, sparse, as leaves without albedo over that background
+ * (a wdas_cloud-style density-only file); files with an albedo grid are read
+ * as before.  opts may be NULL (= cvr_scene_load). */
+enum { CVR_LOAD_DEFAULT_ALBEDO = 1 };
+typedef struct cvr_load_options {
+  uint32_t flags;
+  float default_albedo[3];
+} cvr_load_options;
+int cvr_scene_load_ex(const char* path, int scene_type, const cvr_load_options* opts, cvr_scene** out);
 /* Synthetic proxies for the missing data blobs:
  * "bucky" (32^3 raw), "manix" (256x230x256 VDB-like), "hetvol" (128x128x50),
  * "cloud" (C5: sparse fBm cumulus in a 2048x1024x2048 index box, albedo

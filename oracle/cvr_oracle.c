@@ -118,6 +118,7 @@ typedef struct {
   int32_t kernel;       /* 0 naiveSK, 2 regenerationSK, ... (Config.h Kernel) */
   uint32_t seed_base;   /* RNG seed = seed_base + path_id */
   uint32_t max_segments;/* safety cap (0 = none) */
+  int32_t world_to_aabb;/* Q4: 0 the reference's p - min/extent, 1 fixed (CVR_OPT_WORLD_TO_AABB) */
 } oracle_launch;
 
 typedef struct {
@@ -161,12 +162,13 @@ static inline float tex_albedo(const oracle_medium* m, uint32_t x, uint32_t y, u
 }
 
 typedef struct { int x1, y1, z1; float fx, fy, fz; } tri_t;
-static inline tri_t tri_setup(f3 p, const uint32_t res[3]) {
-  /* DeviceVolume::volumeToGrid: p * (res - 1) */
+/* DeviceVolume::volumeToGrid: p * (res - 1); g = (res - 1), or for the
+ * density with the Q4 fix (res - 1)/extent (see woodcock) */
+static inline tri_t tri_setup_g(f3 p, const float g[3]) {
   tri_t t;
-  float cx = p.x * (float)(res[0] - 1u);
-  float cy = p.y * (float)(res[1] - 1u);
-  float cz = p.z * (float)(res[2] - 1u);
+  float cx = p.x * g[0];
+  float cy = p.y * g[1];
+  float cz = p.z * g[2];
   t.x1 = det_floor_i32(cx);
   t.y1 = det_floor_i32(cy);
   t.z1 = det_floor_i32(cz);
@@ -175,8 +177,12 @@ static inline tri_t tri_setup(f3 p, const uint32_t res[3]) {
   t.fz = cz - (float)t.z1;
   return t;
 }
-static float density_lookup(const oracle_medium* m, f3 p) {
-  tri_t t = tri_setup(p, m->res);
+static inline tri_t tri_setup(f3 p, const uint32_t res[3]) {
+  const float g[3] = {(float)(res[0] - 1u), (float)(res[1] - 1u), (float)(res[2] - 1u)};
+  return tri_setup_g(p, g);
+}
+static float density_lookup_g(const oracle_medium* m, f3 p, const float g[3]) {
+  tri_t t = tri_setup_g(p, g);
   const uint32_t rx = m->res[0], ry = m->res[1], rz = m->res[2];
   uint32_t xa = texel(t.x1, rx), xb = texel(t.x1 + 1, rx);
   uint32_t ya = texel(t.y1, ry), yb = texel(t.y1 + 1, ry);
@@ -189,6 +195,10 @@ static float density_lookup(const oracle_medium* m, f3 p) {
   float a = lerpf(lerpf(d000, d001, t.fx, _fx), lerpf(d010, d011, t.fx, _fx), t.fy, _fy);
   float b = lerpf(lerpf(d100, d101, t.fx, _fx), lerpf(d110, d111, t.fx, _fx), t.fy, _fy);
   return lerpf(a, b, t.fz, _fz);
+}
+static float density_lookup(const oracle_medium* m, f3 p) {
+  const float g[3] = {(float)(m->res[0] - 1u), (float)(m->res[1] - 1u), (float)(m->res[2] - 1u)};
+  return density_lookup_g(m, p, g);
 }
 static f3 albedo_lookup(const oracle_medium* m, f3 p) {
   tri_t t = tri_setup(p, m->res);
@@ -239,12 +249,22 @@ static int aabb_intersect(const oracle_medium* m, f3 o, f3 d, isect_t* is) {
 /* ------------------------------------------------------- Woodcock ------ */
 /* Utilities.cuh:129-155 + Medium.h:135-143.  The density at a tentative
  * point beyond max_t is computed by the reference but never used (the loop
- * condition tests t <= max_t first), so it is not evaluated here. */
+ * condition tests t <= max_t first), so it is not evaluated here.
+ * worldToAABB (Utilities.cuh:129-132) is p - start/range by operator
+ * precedence (Q4, the default).  fix_q4: the intended (p - start)/range, as
+ * the kernels compute it with CVR_OPT_WORLD_TO_AABB 1: c = p - start, then the
+ * grid coordinate c * ((res - 1)/range), one rounding per step. */
 static float woodcock(const oracle_medium* m, f3 o, f3 d, float max_t, xorwow_t* rng,
-                      uint32_t* n_steps, uint32_t* n_density) {
+                      uint32_t* n_steps, uint32_t* n_density, int fix_q4) {
   f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
   f3 ext = sub3(mk3(m->box_max[0], m->box_max[1], m->box_max[2]), bmin);
-  f3 shift = div3(bmin, ext); /* worldToAABB: p - start/range (Q4) */
+  f3 shift = fix_q4 ? bmin : div3(bmin, ext); /* worldToAABB: p - start/range (Q4) */
+  float g[3] = {(float)(m->res[0] - 1u), (float)(m->res[1] - 1u), (float)(m->res[2] - 1u)};
+  if (fix_q4) {
+    g[0] = g[0] / ext.x;
+    g[1] = g[1] / ext.y;
+    g[2] = g[2] / ext.z;
+  }
   float inv = 1.0f / (m->scale * m->max_density);
   float t = 0.0f;
   for (;;) {
@@ -254,7 +274,7 @@ static float woodcock(const oracle_medium* m, f3 o, f3 d, float max_t, xorwow_t*
     if (!(t <= max_t)) break;
     f3 p = mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z));
     f3 c = sub3(p, shift);
-    float rho = m->scale * density_lookup(m, c);
+    float rho = m->scale * density_lookup_g(m, c, g);
     ++*n_density;
     if (!(rho * inv < rng_float(rng))) break;
   }
@@ -445,102 +465,199 @@ static void rng_seeded(xorwow_t* s, uint32_t iteration, uint32_t index, uint32_t
   rng_init(s, (int32_t)h); /* Rng(int) */
 }
 
-/* NaiveVolPTmk_kernel.cuh:20-151 + NaiveVolPTmk::launchRender/extend
- * (RenderKernelLauncher.cu:183-272).  Path id = iteration * tile_px + pixel,
- * as for the other kernels.  d_init: camera ray from the (iteration, pixel,
- * 0) stream, AABB test (a miss adds (1,1,1) to the pixel), GGX at the box
- * before any medium test (Q12; a failed sample drops the path).  Each bounce
- * (d_extend) re-seeds from (iteration, pixel, depth) and first draws three
- * unused numbers (Q12), then runs one naiveSK segment (scatter with -eps).
- * Compaction keeps every live path (Q11 fixed: the reference's
- * `end - begin - 1` drops one live path per bounce).  Flags: bit0 contributed
- * (T), bit1 truncated, bit2 missed the box at init (T = 1), bit3 dropped by a
- * failed GGX sample at init.  n_segments counts d_init plus every d_extend. */
-static void trace_path_mk(const oracle_medium* m, const oracle_launch* L, uint32_t path_id, oracle_path* res) {
-  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
-  const uint32_t image_id = path_id % tile_px;
-  const uint32_t iteration = path_id / tile_px;
+/* NaiveVolPTmk_kernel::d_init (NaiveVolPTmk_kernel.cuh:20-77): camera ray
+ * from the (iteration, pixel, 0) stream, AABB test (a miss adds (1,1,1) to
+ * the pixel), GGX at the box before any medium test (Q12; a failed sample
+ * drops the path).  Returns 0 alive, 1 missed, 2 dropped. */
+typedef struct { f3 o, d, T; } mk_path_t;
+static int mk_init(const oracle_medium* m, const oracle_launch* L, uint32_t iteration, uint32_t image_id,
+                   mk_path_t* p) {
   xorwow_t rng;
   rng_seeded(&rng, iteration, image_id, 0u);
   float px = (float)(image_id % (uint32_t)L->tile_res[0]) + (float)L->offset[0];
   float py = det_floorf((float)image_id / L->tile_res[0]) + (float)L->offset[1];
-  f3 o, d;
-  camera_ray(L, px, py, &rng, &o, &d);
-  f3 T = mk3(1.0f, 1.0f, 1.0f);
-  memset(res, 0, sizeof(*res));
-  res->image_id = image_id;
-  res->n_segments = 1;
+  camera_ray(L, px, py, &rng, &p->o, &p->d);
+  p->T = mk3(1.0f, 1.0f, 1.0f);
   isect_t is;
   is.dist = 0.0f;
   is.normal = mk3(0, 0, 0);
   is.inside = 0;
-  if (!aabb_intersect(m, o, d, &is)) {
+  if (!aabb_intersect(m, p->o, p->d, &is)) return 1;
+  if (is.dist < 0.0f) is.dist = 0.0f; /* clamp to near plane */
+  p->o = add3(p->o, scl3(p->d, is.dist));
+  frame_t fr = frame_from_z(is.normal);
+  f3 dir = frame_to_local(&fr, normalize3(neg3(p->d)));
+  float weight = 1.0f;
+  if (!ggx_sample(m, dir, &rng, &p->d, &weight)) return 2;
+  p->T = scl3(p->T, weight);
+  p->d = frame_to_world(&fr, p->d);
+  p->o = add3(p->o, scl3(p->d, EPS));
+  return 0;
+}
+
+/* One NaiveVolPTmk_kernel::d_extend bounce (NaiveVolPTmk_kernel.cuh:79-151):
+ * re-seed from (iteration, pixel, depth), three unused draws (Q12), one
+ * naiveSK segment (scatter with -eps), roulette.  Returns 0 alive,
+ * 3 escaped (contributes T), 4 died in roulette. */
+static int mk_extend(const oracle_medium* m, const oracle_launch* L, uint32_t iteration, uint32_t image_id,
+                     uint32_t depth, mk_path_t* p, oracle_path* res) {
+  xorwow_t rng;
+  rng_seeded(&rng, iteration, image_id, depth);
+  (void)rng_float(&rng); /* float3 e = rng.getFloat3(), unused */
+  (void)rng_float(&rng);
+  (void)rng_float(&rng);
+  isect_t is;
+  is.dist = 0.0f; /* a fresh SimpleIsect per d_extend */
+  is.normal = mk3(0, 0, 0);
+  is.inside = 0;
+  if (!aabb_intersect(m, p->o, p->d, &is)) return 3;
+  float sampled = 0.0f;
+  int collided = 0;
+  if (is.inside) {
+    sampled = woodcock(m, p->o, p->d, is.dist, &rng, &res->n_steps, &res->n_density, L->world_to_aabb);
+    collided = sampled < is.dist;
+  }
+  if (!collided) {
+    frame_t fr = frame_from_z(is.normal);
+    f3 dir = frame_to_local(&fr, normalize3(neg3(p->d)));
+    p->o = add3(p->o, scl3(p->d, is.dist));
+    float weight = 1.0f;
+    if (ggx_sample(m, dir, &rng, &p->d, &weight)) {
+      p->T = scl3(p->T, weight);
+      p->d = frame_to_world(&fr, p->d);
+      p->o = add3(p->o, scl3(p->d, EPS));
+    }
+  } else {
+    p->o = sub3(add3(p->o, scl3(p->d, sampled)), scl3(p->d, EPS));
+    f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
+    f3 bmax = mk3(m->box_max[0], m->box_max[1], m->box_max[2]);
+    f3 a = albedo_lookup(m, div3(sub3(p->o, bmin), sub3(bmax, bmin)));
+    ++res->n_albedo;
+    p->T = mul3(p->T, a);
+    float e1 = rng_float(&rng);
+    float e2 = rng_float(&rng);
+    p->d = hg_sample(p->d, m->g, e1, e2);
+  }
+  float q = det_fminf(1.0f, det_fmaxf(det_fmaxf(p->T.x, p->T.y), p->T.z));
+  if (rng_float(&rng) > q) return 4;
+  p->T = mk3(p->T.x / q, p->T.y / q, p->T.z / q);
+  return 0;
+}
+
+/* NaiveVolPTmk_kernel.cuh:20-151 + NaiveVolPTmk::launchRender/extend
+ * (RenderKernelLauncher.cu:183-272).  Path id = iteration * tile_px + pixel,
+ * as for the other kernels.  Each bounce (d_extend) re-seeds, so per path the
+ * launches reduce to d_init + d_extend(depth = 0, 1, ...) until the path
+ * ends.  Compaction keeps every live path (Q11 fixed: the reference's
+ * `end - begin - 1` drops one live path per bounce, restated by
+ * oracle_render_mk_reference).  Flags: bit0 contributed (T), bit1 truncated,
+ * bit2 missed the box at init (T = 1), bit3 dropped by a failed GGX sample at
+ * init.  n_segments counts d_init plus every d_extend. */
+static void trace_path_mk(const oracle_medium* m, const oracle_launch* L, uint32_t path_id, oracle_path* res) {
+  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
+  const uint32_t image_id = path_id % tile_px;
+  const uint32_t iteration = path_id / tile_px;
+  mk_path_t p;
+  memset(res, 0, sizeof(*res));
+  res->image_id = image_id;
+  res->n_segments = 1;
+  const int s0 = mk_init(m, L, iteration, image_id, &p);
+  if (s0 == 1) {
     res->flags = 1u | 4u;
     res->T[0] = res->T[1] = res->T[2] = 1.0f;
     return;
   }
-  if (is.dist < 0.0f) is.dist = 0.0f; /* clamp to near plane */
-  o = add3(o, scl3(d, is.dist));
-  {
-    frame_t fr = frame_from_z(is.normal);
-    f3 dir = frame_to_local(&fr, normalize3(neg3(d)));
-    float weight = 1.0f;
-    if (!ggx_sample(m, dir, &rng, &d, &weight)) {
-      res->flags = 8u;
-      return;
-    }
-    T = scl3(T, weight);
-    d = frame_to_world(&fr, d);
-    o = add3(o, scl3(d, EPS));
+  if (s0 == 2) {
+    res->flags = 8u;
+    return;
   }
   for (uint32_t depth = 0;; ++depth) {
     if (L->max_segments && res->n_segments >= L->max_segments) { res->flags |= 2u; break; }
     ++res->n_segments;
-    rng_seeded(&rng, iteration, image_id, depth);
-    (void)rng_float(&rng); /* float3 e = rng.getFloat3(), unused */
-    (void)rng_float(&rng);
-    (void)rng_float(&rng);
-    is.dist = 0.0f; /* a fresh SimpleIsect per d_extend */
-    is.normal = mk3(0, 0, 0);
-    is.inside = 0;
-    if (!aabb_intersect(m, o, d, &is)) {
-      res->flags |= 1u;
-      break;
-    }
-    float sampled = 0.0f;
-    int collided = 0;
-    if (is.inside) {
-      sampled = woodcock(m, o, d, is.dist, &rng, &res->n_steps, &res->n_density);
-      collided = sampled < is.dist;
-    }
-    if (!collided) {
-      frame_t fr = frame_from_z(is.normal);
-      f3 dir = frame_to_local(&fr, normalize3(neg3(d)));
-      o = add3(o, scl3(d, is.dist));
-      float weight = 1.0f;
-      if (ggx_sample(m, dir, &rng, &d, &weight)) {
-        T = scl3(T, weight);
-        d = frame_to_world(&fr, d);
-        o = add3(o, scl3(d, EPS));
-      }
-    } else {
-      o = sub3(add3(o, scl3(d, sampled)), scl3(d, EPS));
-      f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
-      f3 bmax = mk3(m->box_max[0], m->box_max[1], m->box_max[2]);
-      f3 a = albedo_lookup(m, div3(sub3(o, bmin), sub3(bmax, bmin)));
-      ++res->n_albedo;
-      T = mul3(T, a);
-      float e1 = rng_float(&rng);
-      float e2 = rng_float(&rng);
-      d = hg_sample(d, m->g, e1, e2);
-    }
-    float p = det_fminf(1.0f, det_fmaxf(det_fmaxf(T.x, T.y), T.z));
-    if (rng_float(&rng) > p) break;
-    T = mk3(T.x / p, T.y / p, T.z / p);
+    const int e = mk_extend(m, L, iteration, image_id, depth, &p, res);
+    if (e == 3) res->flags |= 1u;
+    if (e != 0) break;
   }
-  res->T[0] = T.x;
-  res->T[1] = T.y;
-  res->T[2] = T.z;
+  res->T[0] = p.T.x;
+  res->T[1] = p.T.y;
+  res->T[2] = p.T.z;
+}
+
+/* naiveMK with the reference's compaction count (quirk Q11 reproduced,
+ * CVR_OPT_MK_COMPACTION 1): NaiveVolPTmk::launchRender/extend
+ * (RenderKernelLauncher.cu:183-272) over `iterations` passes of the tile.
+ * The active list starts as the pixel ids in order (d_init writes
+ * active[img] = img or -1) and thrust::remove_if compacts it stably, so it
+ * stays in ascending pixel order; after each bounce the processed count is
+ * (live paths) - 1: the live path with the highest pixel id is never extended
+ * again.  A bounce that leaves no live path underflows the reference's uint
+ * count (its next launch reads stale entries): returns -2 with the iteration
+ * and bounce in err[0..1].  `out` is the tile accumulator. */
+EXPORT int oracle_render_mk_reference(const oracle_medium* m, const oracle_launch* L, uint32_t iterations,
+                                      float* out, oracle_stats* stats, uint32_t err[2]) {
+  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
+  mk_path_t* st = (mk_path_t*)calloc(tile_px ? tile_px : 1, sizeof(mk_path_t));
+  uint8_t* live = (uint8_t*)calloc(tile_px ? tile_px : 1, 1);
+  if (!st || !live) return -1;
+  oracle_stats sa;
+  memset(&sa, 0, sizeof(sa));
+  int rc = 0;
+  for (uint32_t it = 0; it < iterations && rc == 0; ++it) {
+    for (uint32_t img = 0; img < tile_px; ++img) {
+      const int s0 = mk_init(m, L, it, img, &st[img]);
+      sa.paths++;
+      sa.segments++;
+      live[img] = s0 == 0;
+      if (s0 == 1) { /* d_output[img_id] += (1,1,1,1) */
+        out[4 * (size_t)img + 0] += 1.0f;
+        out[4 * (size_t)img + 1] += 1.0f;
+        out[4 * (size_t)img + 2] += 1.0f;
+        out[4 * (size_t)img + 3] = 1.0f;
+        sa.escaped++;
+      }
+    }
+    uint64_t n_processed = tile_px;
+    for (uint32_t depth = 0; n_processed != 0; ++depth) {
+      uint32_t count = 0, max_id = 0;
+      for (uint32_t img = 0; img < tile_px; ++img) {
+        if (!live[img]) continue;
+        oracle_path r;
+        memset(&r, 0, sizeof(r));
+        const int e = mk_extend(m, L, it, img, depth, &st[img], &r);
+        sa.segments++;
+        sa.steps += r.n_steps;
+        sa.density += r.n_density;
+        sa.albedo += r.n_albedo;
+        if (e == 3) {
+          out[4 * (size_t)img + 0] += st[img].T.x;
+          out[4 * (size_t)img + 1] += st[img].T.y;
+          out[4 * (size_t)img + 2] += st[img].T.z;
+          out[4 * (size_t)img + 3] = 1.0f;
+          sa.escaped++;
+        }
+        if (e == 0) {
+          ++count;
+          max_id = img;
+        } else {
+          live[img] = 0;
+        }
+      }
+      if (count == 0) {
+        if (err) {
+          err[0] = it;
+          err[1] = depth;
+        }
+        rc = -2;
+        break;
+      }
+      n_processed = count - 1u;
+      live[max_id] = 0; /* the compacted list's last entry, dropped by end - begin - 1 */
+    }
+  }
+  free(st);
+  free(live);
+  if (stats) *stats = sa;
+  return rc;
 }
 
 /* ----------------------------------------------------------- path ------ */
@@ -579,7 +696,7 @@ EXPORT void oracle_trace_path(const oracle_medium* m, const oracle_launch* L, ui
     float sampled = 0.0f;
     int collided = 0;
     if (is.inside) {
-      sampled = woodcock(m, o, d, is.dist, &rng, &res->n_steps, &res->n_density);
+      sampled = woodcock(m, o, d, is.dist, &rng, &res->n_steps, &res->n_density, L->world_to_aabb);
       collided = sampled < is.dist;
     }
     if (!collided) {
@@ -789,7 +906,7 @@ EXPORT int oracle_render_thread_bound(const oracle_medium* m, const oracle_launc
         int collided = 0;
         uint32_t ns = 0, nd = 0;
         if (p->is.inside) {
-          sampled = woodcock(m, p->o, p->d, p->is.dist, &p->rng, &ns, &nd);
+          sampled = woodcock(m, p->o, p->d, p->is.dist, &p->rng, &ns, &nd, L->world_to_aabb);
           collided = sampled < p->is.dist;
         }
         st.steps += ns;

@@ -34,7 +34,7 @@ class OracleLaunch(C.Structure):
     _fields_ = [("inv_view", C.c_float * 12), ("raster_to_view", C.c_float * 2),
                 ("full_res", C.c_float * 2), ("tile_res", C.c_float * 2),
                 ("offset", C.c_uint32 * 2), ("kernel", C.c_int32), ("seed_base", C.c_uint32),
-                ("max_segments", C.c_uint32)]
+                ("max_segments", C.c_uint32), ("world_to_aabb", C.c_int32)]
 
 
 class OracleStats(C.Structure):
@@ -70,6 +70,9 @@ def load():
     lib.oracle_render_thread_bound.argtypes = [C.POINTER(OracleMedium), C.POINTER(OracleLaunch), C.c_uint32,
                                                C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.POINTER(OracleStats)]
     lib.oracle_render_thread_bound.restype = C.c_int
+    lib.oracle_render_mk_reference.argtypes = [C.POINTER(OracleMedium), C.POINTER(OracleLaunch), C.c_uint32,
+                                               C.POINTER(C.c_float), C.POINTER(OracleStats), P]
+    lib.oracle_render_mk_reference.restype = C.c_int
     lib.oracle_rng_stream.argtypes = [C.c_int32, C.c_uint32, P, P]
     lib.oracle_rng_state.argtypes = [C.c_int32, P]
     lib.oracle_density.argtypes = [C.POINTER(OracleMedium), P]
@@ -142,7 +145,9 @@ class Oracle:
 
     @staticmethod
     def launch(inv_view, r2v, full_res, tile_res, offset=(0, 0), kernel=0, seed_base=0,
-               max_segments=1 << 20) -> OracleLaunch:
+               max_segments=1 << 20, world_to_aabb=0) -> OracleLaunch:
+        """world_to_aabb: quirk Q4, 0 the reference's p - min/extent, 1 the fix
+        (CVR_OPT_WORLD_TO_AABB)."""
         L = OracleLaunch()
         L.inv_view[:] = [float(v) for v in inv_view]
         L.raster_to_view[:] = [float(v) for v in r2v]
@@ -152,6 +157,7 @@ class Oracle:
         L.kernel = kernel
         L.seed_base = seed_base
         L.max_segments = max_segments
+        L.world_to_aabb = world_to_aabb
         return L
 
     def trace_paths(self, L: OracleLaunch, first: int, count: int) -> np.ndarray:
@@ -181,6 +187,20 @@ class Oracle:
                                                  out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st))
         assert rc == 0
         return out, st
+
+    def render_mk_reference(self, L: OracleLaunch, iterations: int):
+        """naiveMK with the reference's compaction count (quirk Q11 reproduced,
+        cvr_oracle.c oracle_render_mk_reference).  Returns (tile accumulator,
+        stats, None) or (partial accumulator, stats, (iteration, bounce)) when a
+        bounce leaves no live path (the reference's count underflows)."""
+        w, h = int(L.tile_res[0]), int(L.tile_res[1])
+        out = np.zeros((h, w, 4), np.float32)
+        st = OracleStats()
+        err = np.zeros(2, np.uint32)
+        rc = self.lib.oracle_render_mk_reference(C.byref(self.m), C.byref(L), iterations,
+                                                 out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st), _p(err))
+        assert rc in (0, -2)
+        return out, st, (None if rc == 0 else (int(err[0]), int(err[1])))
 
     def density_at(self, p):
         p = np.asarray(p, np.float32)
