@@ -1367,13 +1367,19 @@ int cvr_trace_launch(cvr_ctx* c, cvr_path_record* out, uint64_t n_out) {
   const uint64_t grid = c->grid_override ? c->grid_override : (uint64_t)(sparse ? c->wpool_grid_sparse : c->wpool_grid);
   const size_t pid_bytes = (size_t)grid * cvr::wpool_slots(wpool_waves_for(c, sparse), sparse) * sizeof(uint32_t);
   const size_t rec_bytes = (size_t)count * sizeof(cvr_path_record);
+  // the traced launch splats into a scratch framebuffer, not the context's
+  const size_t out_bytes = (size_t)c->tile_w * c->tile_h * sizeof(float4);
+  const size_t out_at = (pid_bytes + rec_bytes + 16 + 255) & ~(size_t)255;
   char* d = nullptr;
-  HIP_TRY(c, hipMalloc(&d, pid_bytes + rec_bytes + 16));
-  hipError_t e = hipMemsetAsync(d, 0, pid_bytes + rec_bytes + 16, c->stream);
+  HIP_TRY(c, hipMalloc(&d, out_at + out_bytes));
+  hipError_t e = hipMemsetAsync(d, 0, out_at + out_bytes, c->stream);
   if (e == hipSuccess) {
+    float4* saved_out = c->d_out;
+    c->d_out = reinterpret_cast<float4*>(d + out_at);
     c->d_rec_active = d + pid_bytes;
     r = cvr_launch_render(c);
     c->d_rec_active = nullptr;
+    c->d_out = saved_out;
     if (!r) {
       // the kernel writes path p's record at p - L.path_first: a contiguous
       // shard (no block order) moved path_first to the shard's first id

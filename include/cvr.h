@@ -267,7 +267,8 @@ int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_recor
  * (cvr_set_path_range; n_out must equal the range's length).  image_id, flags,
  * T and n_segments are filled (n_steps, n_density, n_albedo stay 0: the wave
  * pool counts those per lane); ids outside a block shard stay zero.
- * Synchronous. */
+ * Synchronous.  The traced launch splats into a scratch buffer (the context's
+ * output is untouched); cvr_get_stats afterwards reports its counters. */
 int cvr_trace_launch(cvr_ctx* ctx, cvr_path_record* out, uint64_t n_out);
 /* Diagnostic builds (-DCVR_STAMPS=1) only: per-phase cycle counters of the
  * persistent kernel {event cycles, track cycles, event phases, track

@@ -45,6 +45,13 @@ def test_two_ranks_one_gpu_bench_step_equals_single_render(cvr, tmp_path, shard,
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
     if shard == "paths":
         assert line["weak"]["value"] > 0
+    # the scaling run's self-diagnosis (bench.py rank_diagnostics)
+    rk = line["ranks"]
+    assert rk["world_size_reported"] == 2 and rk["backend"] == "gloo" and rk["streams_per_process"] >= 1
+    for k in ("kernel_ms_min_max", "reduce_scatter_ms_min_max", "slice_copy_ms_min_max"):
+        lo, hi = rk[k]
+        assert 0 < lo <= hi, k
+    assert rk["image_check"]["match"], rk["image_check"]
     img = np.load(out)
     scene = cvr.Scene.synthetic("manix")
     ctx = cvr.Context(0, "regenerationSK")
