@@ -70,9 +70,17 @@ __device__ __forceinline__ float opaque_s(float x) {
 // 122 at 5.  The pool size matters: lanes step only while the pool holds
 // track-ready paths besides the events waiting for a batch (93 slots instead
 // of 118 at 4 waves cost 13% on C2).
+// LDS is handed to workgroups in 1280-byte granules (measured, tools/census.hip:
+// one-wave workgroups of 7680 B fit 20 per CU, of 7936 / 8064 / 8192 B only 18,
+// although the occupancy API answers 20 for all of them; 10240 B fit 16).  A
+// budget of 163840 / 20 = 8192 B therefore ran 4.5 waves per SIMD, not 5.
+#ifndef CVR_LDS_GRANULE
+#define CVR_LDS_GRANULE 1280
+#endif
 template <int kWaves, bool kSplit>
 struct PoolSize {
-  static constexpr int kBudget = 163840 / (4 * kWaves);  // LDS bytes per one-wave workgroup
+  // LDS bytes per one-wave workgroup
+  static constexpr int kBudget = 163840 / (4 * kWaves) / CVR_LDS_GRANULE * CVR_LDS_GRANULE;
   static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
 #ifdef CVR_WPOOL_SLOTS  // experiment builds: a smaller pool
   static constexpr int value = CVR_WPOOL_SLOTS;
