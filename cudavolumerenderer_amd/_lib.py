@@ -28,7 +28,7 @@ SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4, "VdbSpa
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
-OPT_WORLD_TO_AABB, OPT_MK_COMPACTION = 18, 19
+OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES = 18, 19, 20
 
 
 class CvrError(RuntimeError):

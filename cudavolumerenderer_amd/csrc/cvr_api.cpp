@@ -110,6 +110,7 @@ struct cvr_ctx {
   float4* d_pool_T = nullptr;       // wave-pool scheduler: event-only slot part (LaunchParams::pool_T)
   size_t pool_T_n = 0;
   uint32_t n_queues = 8;            // work-order bands (one per XCD)
+  uint32_t subqueues = 8;           // wave pool: queues per band (CVR_OPT_SUBQUEUES)
   int order = 2;                    // 1: pixel-block/sample-inner order when the launch allows it; 2: blocks
                                     // in 2-D Morton order within each band
   // cached Morton permutation of the launch's blocks (order 2), for the block layout in zkey
@@ -157,14 +158,14 @@ struct cvr_ctx {
   cvr_stats last{};
 };
 
-// d_work layout: 8 queue heads one 64-byte line apart, then 16 u64 stats
-// (single-kernel launches / wavefront events, wavefront track), then 8 u64
-// diagnostic counters (CVR_STAMPS builds).
 #ifndef CVR_TAILSTAMPS
 #define CVR_TAILSTAMPS 0
 #endif
-constexpr size_t kWorkQueues = 0, kWorkStats = 512, kWorkDebug = 640,
-                 kWorkBytes = CVR_TAILSTAMPS ? 1024 + (size_t)80 * 65536 : 1024;
+using cvr::kWorkDebug;
+using cvr::kWorkQueues;
+using cvr::kWorkStats;
+// d_work layout: cvr_kernels.h (stats, debug counters, queue heads)
+constexpr size_t kWorkBytes = cvr::kWorkBytesBase + (CVR_TAILSTAMPS ? (size_t)(80 + 384) * 65536 : 0);
 
 #define HIP_TRY(ctx, expr)                                                                         \
   do {                                                                                                  \
@@ -299,17 +300,22 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
       L.n_blocks = L.n_blocks > c->shard_rank ? (L.n_blocks - c->shard_rank + c->shard_world - 1) / c->shard_world : 0;
       L.path_count = L.n_blocks * 64u * L.samples;
     }
-    L.n_queues = c->n_queues < L.n_blocks ? c->n_queues : L.n_blocks;
-    if (L.n_queues == 0) L.n_queues = 1;
+    uint32_t bands = c->n_queues < L.n_blocks ? c->n_queues : L.n_blocks;
+    if (bands == 0) bands = 1;
+    // sub-queues per band: the wave pool only, each with at least one block
+    uint32_t sub = scheduler_for(c) == 3 ? c->subqueues : 1u;
+    while (sub > 1 && bands * sub > L.n_blocks) --sub;
+    L.sub = sub;
+    L.n_queues = bands * sub;
   } else {
     L.order = 0;
     L.samples = 0;
     L.blocks_x = 0;
     L.n_blocks = 0;
     L.n_queues = 1;
+    L.sub = 1;
   }
-  for (uint32_t q = 0; q <= 8; ++q)
-    L.qbeg[q] = q <= L.n_queues ? (uint32_t)((uint64_t)L.n_blocks * q / L.n_queues) : L.n_blocks;
+  L.div_queues = make_fastdiv(L.n_queues);
   L.block_perm = (L.order == 1 && c->d_block_perm && c->block_perm_n == L.n_blocks) ? c->d_block_perm : nullptr;
   L.div_tile_px = make_fastdiv(L.tile_px);
   L.div_tile_w = make_fastdiv(L.tile_w);
@@ -331,6 +337,13 @@ cvr::MediumParams launch_medium(const cvr_ctx* c) {
   }
   return m;
 }
+
+// First block of queue q of a launch (LaunchParams::n_queues; cvr_walk.h queue_blocks_begin).
+uint32_t queue_begin(const cvr::LaunchParams& L, uint32_t q) {
+  return (uint32_t)((uint64_t)L.n_blocks * q / L.n_queues);
+}
+// First block of XCD band b (n_queues / sub bands of sub queues each).
+uint32_t band_begin(const cvr::LaunchParams& L, uint32_t b) { return queue_begin(L, b * L.sub); }
 
 int check_ready(cvr_ctx* c) {
   if (!c->have_medium) return set_err(&c->err, CVR_ERR_STATE, "medium not set (cvr_set_medium)");
@@ -978,8 +991,9 @@ int cvr_launch_blocks(const cvr_ctx* c, uint32_t* n_blocks, uint32_t* n_queues, 
   compute_range(c, &first, &count);
   fill_launch(c, L, first, count);
   *n_blocks = L.order == 1 ? L.n_blocks : 0;
-  *n_queues = L.n_queues;
-  for (int q = 0; q < 9; ++q) qbeg[q] = L.qbeg[q];
+  const uint32_t bands = L.n_queues / L.sub;
+  *n_queues = bands;
+  for (uint32_t q = 0; q < 9; ++q) qbeg[q] = q <= bands ? band_begin(L, q) : L.n_blocks;
   return CVR_OK;
 }
 
@@ -1055,6 +1069,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
     case CVR_OPT_QUEUES:
       if (v < 1 || v > 8) return set_err(&c->err, CVR_ERR_INVALID, "queues must be 1..8");
       c->n_queues = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_SUBQUEUES:
+      if (v < 1 || v > 8) return set_err(&c->err, CVR_ERR_INVALID, "subqueues must be 1..8");
+      c->subqueues = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_WAVES:
       if (v != 3 && v != 4 && v != 5 && v != 6 && v != 8)
@@ -1138,14 +1156,14 @@ static uint32_t spread_bits16(uint32_t v) {  // bit i -> bit 2i
 // layout, kept on the device.
 static int ensure_zorder(cvr_ctx* c, cvr::LaunchParams& L) {
   if (L.order != 1 || L.block_perm || c->order != 2 || L.n_blocks == 0) return CVR_OK;
-  const uint64_t key[5] = {L.n_blocks, L.n_queues, L.blk_off, L.blk_stride, L.blocks_x};
+  const uint64_t key[5] = {L.n_blocks, (uint64_t)L.n_queues / L.sub, L.blk_off, L.blk_stride, L.blocks_x};
   if (!c->d_zperm || memcmp(key, c->zkey, sizeof(key)) != 0) {
     const uint32_t nb = L.n_blocks;
     std::vector<uint32_t>& perm = c->h_zperm;
     perm.resize(nb);
     std::vector<std::pair<uint32_t, uint32_t>> code(nb);
-    for (uint32_t q = 0; q < L.n_queues; ++q) {
-      const uint32_t a = L.qbeg[q], e = L.qbeg[q + 1];
+    for (uint32_t q = 0; q < L.n_queues / L.sub; ++q) {  // Morton order within each XCD band
+      const uint32_t a = band_begin(L, q), e = band_begin(L, q + 1);
       for (uint32_t b = a; b < e; ++b) {
         const uint32_t tb = L.blk_off + b * L.blk_stride;
         const uint32_t bx = tb % L.blocks_x, by = tb / L.blocks_x;
@@ -1196,7 +1214,7 @@ int cvr_launch_render(cvr_ctx* c) {
                                                       c->wpool_grid_sparse}));
   uint64_t units_max = L.order ? 0 : count;
   for (uint32_t q = 0; L.order && q < L.n_queues; ++q)
-    units_max = std::max<uint64_t>(units_max, (uint64_t)(L.qbeg[q + 1] - L.qbeg[q]) * 64u * L.samples);
+    units_max = std::max<uint64_t>(units_max, (uint64_t)(queue_begin(L, q + 1) - queue_begin(L, q)) * 64u * L.samples);
   if (first + count > 0xFFFFFFFFull || units_max + waves_max * L.chunk > 0xFFFFFFFFull)
     return set_err(&c->err, CVR_ERR_INVALID, "path range [%llu, +%llu) overflows the 32-bit path ids / queue heads",
                    (unsigned long long)first, (unsigned long long)count);
@@ -1335,7 +1353,13 @@ int cvr_debug_counters(cvr_ctx* c, uint64_t out[16]) {
 int cvr_debug_tailstamps(cvr_ctx* c, uint64_t* out, size_t n_waves) {
   if (!c || !out || n_waves > 65536) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "bad argument");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  HIP_TRY(c, hipMemcpy(out, c->d_work + kWorkStats + 64 * 8, n_waves * 80, hipMemcpyDeviceToHost));
+  HIP_TRY(c, hipMemcpy(out, c->d_work + cvr::kWorkBytesBase, n_waves * 80, hipMemcpyDeviceToHost));
+  return CVR_OK;
+}
+// the drain timelines (48 u64 per wave) that follow the stamps of the launch's `grid` waves
+int cvr_debug_tailtimeline(cvr_ctx* c, uint64_t* out, size_t grid) {
+  if (!c || !out || grid > 65536) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "bad argument");
+  HIP_TRY(c, hipMemcpy(out, c->d_work + cvr::kWorkBytesBase + grid * 80, grid * 48 * 8, hipMemcpyDeviceToHost));
   return CVR_OK;
 }
 #endif

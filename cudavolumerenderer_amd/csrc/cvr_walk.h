@@ -199,13 +199,17 @@ struct LaunchParams {
   // path ids in sample-major order from one queue.  order 1: 8x8-pixel
   // blocks with all their samples back to back (path_first must be a
   // multiple of tile_px, path_count = samples * tile_px, tile dims multiples
-  // of 8); the block range is split into n_queues contiguous bands, one
-  // queue each, so that the waves of one XCD share one band (its L2).
+  // of 8); the block range is split into n_queues / sub contiguous bands, one
+  // per XCD, so that the waves of one XCD share one band (its L2), and each
+  // band into `sub` contiguous sub-queues (the wave pool: more queue heads,
+  // so that small dequeue chunks do not contend on one atomic per XCD).
+  // Queue q holds blocks [n_blocks q / n_queues, n_blocks (q+1) / n_queues).
   uint32_t order;
   uint32_t samples;       // path_count / tile_px (order 1)
   uint32_t blocks_x;      // tile_w / 8
   uint32_t n_blocks;      // blocks of this launch: tile_px / 64 (or the block shard's share)
-  uint32_t n_queues;      // 1..8
+  uint32_t n_queues;      // queues in all: bands (1..8) * sub
+  uint32_t sub;           // sub-queues per band (1..8)
   // Block shard (cvr_set_block_shard): this launch's blocks are the tile's
   // blocks blk_off, blk_off + blk_stride, ...; local block b is tile block
   // blk_off + b * blk_stride (0 / 1: the whole tile).
@@ -214,13 +218,14 @@ struct LaunchParams {
   // launch is block_perm[b] (a permutation of [0, n_blocks)), e.g. costly
   // blocks first so that the launch does not end on their long paths.
   const uint32_t* block_perm;
-  uint32_t qbeg[9];       // first block of each queue's band (order 1), qbeg[n_queues] = n_blocks
-  FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x;  // by tile_px, tile_w, 64*samples, blocks_x
+  // by tile_px, tile_w, 64*samples, blocks_x, n_queues
+  FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x, div_queues;
 };
 
 // Map the u-th work unit of queue q to a path id (order 1), see LaunchParams.
+// n_blocks * q < 2^24 (n_blocks <= 2^18, q <= 64).
 CVR_DEV uint32_t queue_blocks_begin(const LaunchParams& L, uint32_t q) {
-  return L.qbeg[q];  // n_blocks * q / n_queues
+  return fastdiv(L.n_blocks * q, L.div_queues);  // n_blocks * q / n_queues
 }
 CVR_DEV uint32_t queue_units(const LaunchParams& L, uint32_t q) {
   if (L.order == 0) return q == 0 ? L.path_count : 0u;

@@ -244,7 +244,12 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   uint32_t c_steps = 0, c_fetch = 0;
   if (lane < (uint32_t)STAT_COUNT) S.cnt[lane] = 0u;
   uint32_t n_over = 0;  // wave-uniform: segments whose last Woodcock step passed max_t
-  Cursor cur{0, 0, 0, (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % L.n_queues, false};
+  // home queue: the XCD's band, and within it sub-queue (workgroup / 8) mod sub
+  // (workgroups are dealt round-robin over the 8 XCDs)
+  Cursor cur{0, 0, 0,
+             ((__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % (L.n_queues / L.sub)) * L.sub +
+                 (blockIdx.x >> 3) % L.sub,
+             false};
   const uint32_t batch = L.batch;  // TRACK: swap finished segments once this many lanes are idle
   // wave-uniform list state
   uint32_t ready_head = 0, n_ready = 0, n_lb = 0, n_lc = 0;
@@ -268,10 +273,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   unsigned long long t_regen = 0;
 #endif
 #if CVR_TAILSTAMPS
-  // start, first track iteration, queues exhausted, end (s_memrealtime, 100 MHz); track iterations,
-  // event batches (total, after exhaustion); lane-steps after exhaustion
+  // start, queues exhausted, end (s_memrealtime, 100 MHz); event batches (total, after
+  // exhaustion); lane-steps after exhaustion (nothing in the track loop: the stamps would
+  // perturb its registers)
   const unsigned long long ts_start = __builtin_amdgcn_s_memrealtime();
-  unsigned long long ts_track = 0, ts_ex = 0, ts_n_tr = 0, ts_n_ev = 0, ts_n_tr_ex = 0, ts_n_ev_ex = 0;
+  unsigned long long ts_ex = 0, ts_n_ev = 0, ts_n_ev_ex = 0, ts_bstart = 0;
   uint32_t ts_steps_ex = 0;
 #endif
   for (;;) {
@@ -338,11 +344,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
       ++st[3];
 #endif
-#if CVR_TAILSTAMPS
-      if (ts_track == 0) ts_track = __builtin_amdgcn_s_memrealtime();
-      ++ts_n_tr;
-      if (cur.exhausted) ++ts_n_tr_ex;
-#endif
 #pragma unroll
       for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
         // woodcock_step_core with both draws taken up front: a step that
@@ -384,7 +385,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
 #if CVR_TAILSTAMPS
     ++ts_n_ev;
-    if (cur.exhausted) ++ts_n_ev_ex;
+    if (cur.exhausted) ts_bstart = __builtin_amdgcn_s_memrealtime();
 #endif
     // Event-code view of the medium: its BSDF / box / albedo fields pass
     // through opaque_s per batch, so values derived from them (HG and box
@@ -626,6 +627,20 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       t_mark = now;
     }
 #endif
+#if CVR_TAILSTAMPS
+    // drain timeline: per batch after exhaustion, (start - exhaustion) | batch duration << 32 |
+    // paths filed as boundary events << 48 | collisions << 56 (10 ns units)
+    if (ts_bstart) {
+      if (ts_n_ev_ex < 48u && lane == 0u) {
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        (L.stats + kStampWord + (size_t)gridDim.x * 10)[(size_t)blockIdx.x * 48 + ts_n_ev_ex] =
+            ((ts_bstart - ts_ex) & 0xFFFFFFFFull) | (min(now - ts_bstart, 0xFFFFull) << 32) |
+            ((unsigned long long)min(n_lb, 255u) << 48) | ((unsigned long long)min(n_ready, 255u) << 56);
+      }
+      ++ts_n_ev_ex;
+      ts_bstart = 0;
+    }
+#endif
   }
 
   // ---- counters ------------------------------------------------------------
@@ -648,8 +663,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     for (int off = 32; off > 0; off >>= 1) sx += __shfl_xor(sx, off);
     const unsigned long long ts_end = __builtin_amdgcn_s_memrealtime();
     const unsigned long long hw = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
-    const unsigned long long v[10] = {ts_start, ts_track, ts_ex, ts_end, ts_n_tr, ts_n_ev, ts_n_tr_ex, ts_n_ev_ex, sx, hw};
-    if (lane < 10u) L.stats[64 + (size_t)blockIdx.x * 10 + lane] = v[lane];
+    const unsigned long long v[10] = {ts_start, 0ull, ts_ex, ts_end, 0ull, ts_n_ev, 0ull, ts_n_ev_ex, sx, hw};
+    if (lane < 10u) L.stats[kStampWord + (size_t)blockIdx.x * 10 + lane] = v[lane];
   }
 #endif
 #if CVR_STAMPS

@@ -98,6 +98,9 @@ typedef enum {
                                  (operator precedence, Utilities.cuh:129-132); 1 the intended
                                  (p - min)/extent, computed as fma(p, 1/extent, -min/extent).  The two
                                  agree for the unit box of VDB/Raw/MHD scenes. */
+  CVR_OPT_SUBQUEUES = 20,      /* wave-pool scheduler: work queues per XCD band (1..8, default 8), each
+                                 over a contiguous part of the band, so that small dequeue chunks do not
+                                 contend on one head.  Scheduling only. */
   CVR_OPT_MK_COMPACTION = 19   /* quirk Q11, naiveMK only: 0 (default) every live path is extended
                                  until it ends; 1 the reference's compaction count end - begin - 1
                                  (RenderKernelLauncher.cu:266-271): after every bounce the live path

@@ -55,31 +55,32 @@ def main():
         c.clear_output()
         c.launch_render()
         st = c.stats()
-    nw = 65536
+    nw = cu * 4 * (4 if scene.is_sparse else 5)  # the wave-pool grid (one wave per workgroup)
     buf = (C.c_uint64 * (nw * 10))()
     lib.cvr_debug_tailstamps(c._h, buf, nw)
     s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 10).astype(np.int64)
-    s = s[s[:, 0] > 0]
     n = len(s)
     t0 = s[:, 0].min()
     us = lambda x: (x - t0) / 100.0  # 100 MHz -> us
-    start, trk, ex, end = us(s[:, 0]), us(s[:, 1]), us(s[:, 2]), us(s[:, 3])
-    n_tr, n_ev, n_tr_ex, n_ev_ex, sx, xcc = s[:, 4], s[:, 5], s[:, 6], s[:, 7], s[:, 8], s[:, 9]
+    start, ex, end = us(s[:, 0]), us(s[:, 2]), us(s[:, 3])
+    n_ev, n_ev_ex, sx, xcc = s[:, 5], s[:, 7], s[:, 8], s[:, 9]
+    late = start > 0.5 * end.max()  # workgroups admitted only when others left (grid > residency)
+    print(f"waves that started after half the span: {late.sum()}")
     q = lambda v: " ".join(f"{np.percentile(v, p):8.1f}" for p in (0, 10, 50, 90, 99, 100))
     print(f"{a.scene} {W}x{H} {a.iters} it shard 1/{a.shard}: {n} waves, kernel {st.kernel_ms:.3f} ms (events), "
           f"steps {st.steps}, paths {st.paths}")
     print("                 percentiles  0      10      50      90      99     100 (us from first wave start)")
     print(f"start          {q(start)}")
-    print(f"first track    {q(trk)}")
     print(f"exhausted      {q(ex)}")
     print(f"end            {q(end)}")
     print(f"end-exhausted  {q(end - ex)}")
     span = end.max()
     print(f"span {span:.1f} us; all waves exhausted at {ex.max():.1f} us; first wave ends {end.min():.1f} us")
     tot_steps = float(st.steps)
-    print(f"lane-steps after exhaustion: {sx.sum() / tot_steps:.4f} of all; track iterations after exhaustion "
-          f"{n_tr_ex.sum() / n_tr.sum():.4f}, lane fill there {sx.sum() / max(n_tr_ex.sum(), 1) / 4 / 64:.3f} "
-          f"vs before {(tot_steps - sx.sum()) / max((n_tr - n_tr_ex).sum(), 1) / 4 / 64:.3f}")
+    t_ex0 = ex.min()
+    print(f"lane-steps after this wave's exhaustion: {sx.sum() / tot_steps:.4f} of all; wave-time after "
+          f"exhaustion {(end - ex).sum() / (end - start).sum():.4f} of all wave-time; ideal tail at the "
+          f"pre-exhaustion step rate {sx.sum() / tot_steps * t_ex0:.1f} us vs actual {span - t_ex0:.1f} us")
     print(f"event batches after exhaustion {n_ev_ex.sum() / n_ev.sum():.4f} ({n_ev_ex.mean():.1f} per wave, "
           f"{n_ev.mean():.1f} total per wave)")
     # active waves over time
@@ -87,6 +88,20 @@ def main():
     act = [(np.sum((start <= g) & (end > g))) for g in grid]
     print("waves alive over time (us: count):")
     print("  " + "  ".join(f"{g:.0f}:{v}" for g, v in zip(grid[::2], act[::2])))
+    # drain timelines of the last waves to end
+    lib.cvr_debug_tailtimeline.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t]
+    tl = (C.c_uint64 * (n * 48))()
+    lib.cvr_debug_tailtimeline(c._h, tl, n)
+    tl = np.frombuffer(tl, dtype=np.uint64).reshape(n, 48)
+    order = np.argsort(-end)
+    for w in order[:4]:
+        print(f"  wave {w} (xcc {xcc[w]}): exhausted {ex[w]:.1f} end {end[w]:.1f} us, {n_ev_ex[w]} batches after:")
+        row = []
+        for k in range(min(int(n_ev_ex[w]), 48)):
+            v = int(tl[w, k])
+            row.append(f"{(v & 0xFFFFFFFF) / 100:.1f}+{((v >> 32) & 0xFFFF) / 100:.1f}us b{(v >> 48) & 255} "
+                       f"r{(v >> 56) & 255}")
+        print("    " + " | ".join(row))
     for x in range(8):
         m = xcc == x
         if m.any():

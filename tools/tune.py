@@ -82,6 +82,8 @@ def main():
             c.set_option(cvr.OPT_ORDER, d["order"])
         if "queues" in d:
             c.set_option(cvr.OPT_QUEUES, d["queues"])
+        if "sub" in d:
+            c.set_option(cvr.OPT_SUBQUEUES, d["sub"])
         if "waves" in d:
             c.set_option(cvr.OPT_WAVES, d["waves"])
         if "batch" in d:
