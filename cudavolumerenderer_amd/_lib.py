@@ -28,7 +28,7 @@ SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4, "VdbSpa
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
-OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES = 18, 19, 20
+OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT = 18, 19, 20, 22, 23
 
 
 class CvrError(RuntimeError):
@@ -121,6 +121,7 @@ def load() -> C.CDLL:
         "cvr_share_medium": (I32, [P, P]),
         "cvr_trace_launch": (I32, [P, P, U64]),
         "cvr_image_to_host": (I32, [P, P, C.c_size_t, C.c_float, P]),
+        "cvr_blocks_to_host": (I32, [P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float, P]),
         "cvr_launch_blocks": (I32, [P, P, P, P]),
         "cvr_set_seed": (I32, [P, U32]),
         "cvr_get_seed": (I32, [P, C.POINTER(U32)]),
@@ -202,6 +203,15 @@ def image_to_host(device_ptr: int, host_ptr: int, n_floats: int, scale: float, s
     pinned or registered host memory (cvr_image_to_host; asynchronous)."""
     _check(load().cvr_image_to_host(C.c_void_p(device_ptr), C.c_void_p(host_ptr), n_floats, scale,
                                     C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
+def blocks_to_host(device_ptr: int, host_ptr: int, width: int, height: int, rank: int, world: int, scale: float,
+                   stream_ptr: Optional[int]):
+    """The pixels of block shard (rank, world) of a width x height float4
+    image, divided by scale, stored by a kernel on `stream_ptr` at their places
+    in the full pinned/registered host image (cvr_blocks_to_host; asynchronous)."""
+    _check(load().cvr_blocks_to_host(C.c_void_p(device_ptr), C.c_void_p(host_ptr), width, height, rank, world,
+                                     scale, C.c_void_p(stream_ptr) if stream_ptr else None))
 
 
 def write_hdr(path: str, rgba: np.ndarray):

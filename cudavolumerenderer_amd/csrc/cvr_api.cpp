@@ -111,6 +111,7 @@ struct cvr_ctx {
   size_t pool_T_n = 0;
   uint32_t n_queues = 8;            // work-order bands (one per XCD)
   uint32_t subqueues = 8;           // wave pool: queues per band (CVR_OPT_SUBQUEUES)
+  int drain = -1;                   // wave pool: drain-mode event trigger (CVR_OPT_DRAIN; -1 = 1)
   int order = 2;                    // 1: pixel-block/sample-inner order when the launch allows it; 2: blocks
                                     // in 2-D Morton order within each band
   // cached Morton permutation of the launch's blocks (order 2), for the block layout in zkey
@@ -123,6 +124,7 @@ struct cvr_ctx {
   uint32_t chunk = 0;  // paths per wave dequeue; 0: auto (wave pool: 64..256 by the launch's size, others 256)
   uint32_t ev_thresh = 56;
   uint32_t grid_override = 0;
+  uint32_t inflight = 1;  // CVR_OPT_INFLIGHT: renders the caller keeps in flight (wave-pool grid rule)
   int scatter_eps = -1;
   int rng_binding = 0;  // CVR_OPT_RNG_BINDING
   int world_to_aabb = 0;  // CVR_OPT_WORLD_TO_AABB (Q4)
@@ -210,6 +212,25 @@ bool morton_for(const cvr_ctx* c) { return c->morton > 0; }
 int wpool_waves_for(const cvr_ctx* c, bool sparse) {
   if (c->wpool_waves) return c->wpool_waves;
   return sparse ? 4 : 5;
+}
+
+// Wave-pool grid of a launch of n_paths (one wave per workgroup): CVR_OPT_GRID,
+// else the occupancy grid, of which a small launch takes a part.  A launch of
+// fewer than 64 paths per wave (C1: 262 K paths) ends mostly in ramp-up and
+// ramp-down at the full grid: half the grid alone, a quarter with renders in
+// flight (the other renders fill the rest; profiles/round2/overlap_c1.log:
+// 0.228 vs 0.287 ms alone, 0.094 vs 0.149 ms per render with three in flight).
+// With renders in flight (CVR_OPT_INFLIGHT > 1) a launch of fewer than 1024
+// paths per wave (an 8-GPU block shard of C2) takes half the grid, so each
+// wave gets twice the paths (1/8 shard 0.700 vs 0.735 ms per render,
+// profiles/round2/overlap_small_shards.log); alone the full grid is faster.
+uint32_t wpool_launch_grid(const cvr_ctx* c, uint64_t n_paths) {
+  if (c->grid_override) return c->grid_override;
+  const uint32_t full = (uint32_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
+  const uint32_t half = std::max(1u, full / 2), quarter = std::max(1u, full / 4);
+  if (n_paths < 64ull * full) return c->inflight > 1 ? quarter : half;
+  if (c->inflight > 1 && n_paths < 1024ull * full) return half;
+  return full;
 }
 
 int ensure_device(cvr_ctx* c) {
@@ -1074,6 +1095,14 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       if (v < 1 || v > 8) return set_err(&c->err, CVR_ERR_INVALID, "subqueues must be 1..8");
       c->subqueues = (uint32_t)v;
       return CVR_OK;
+    case CVR_OPT_INFLIGHT:
+      if (v < 1 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "inflight must be 1..64");
+      c->inflight = (uint32_t)v;
+      return CVR_OK;
+    case CVR_OPT_DRAIN:
+      if (v < -1 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "drain must be -1..64");
+      c->drain = (int)v;
+      return CVR_OK;
     case CVR_OPT_WAVES:
       if (v != 3 && v != 4 && v != 5 && v != 6 && v != 8)
         return set_err(&c->err, CVR_ERR_INVALID, "waves must be 3, 4, 5, 6 or 8");
@@ -1200,10 +1229,12 @@ int cvr_launch_render(cvr_ctx* c) {
     // wave, 64..256 paths.  Small launches (block shards of a multi-GPU render)
     // then end with the waves' last chunks evenly spread (C2 shard 1/8 on one
     // GPU: 1.09 ms at 64 vs 1.18 at 256; the whole C2 launch keeps 256).
-    const uint64_t grid =
-        c->grid_override ? (uint64_t)c->grid_override : (uint64_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
+    const uint64_t grid = wpool_launch_grid(c, L.path_count);
     const uint64_t per_wave = grid ? (uint64_t)L.path_count / grid : 0;
     L.chunk = per_wave >= 2048 ? 256u : per_wave >= 1024 ? 128u : 64u;
+  }
+  if (scheduler_for(c) == 3) {
+    L.drain = (uint32_t)(c->drain < 0 ? 1 : c->drain);
   }
   // The persistent schedulers' u32 queue heads run past a queue's end by at
   // most one chunk per wave before every wave sees the queue exhausted
@@ -1246,8 +1277,7 @@ int cvr_launch_render(cvr_ctx* c) {
   } else if (scheduler_for(c) == 3) {
     const bool sparse = c->m.leaves != nullptr;
     const int waves = wpool_waves_for(c, sparse);
-    const uint32_t grid =
-        c->grid_override ? c->grid_override : (uint32_t)(sparse ? c->wpool_grid_sparse : c->wpool_grid);
+    const uint32_t grid = wpool_launch_grid(c, L.path_count);
     const size_t need = (size_t)grid * cvr::wpool_slots(waves, sparse);
     if (need > c->pool_T_n) {
       if (c->d_pool_T) (void)hipFree(c->d_pool_T);
@@ -1296,6 +1326,24 @@ int cvr_clear_output(cvr_ctx* c) {
   if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
   if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
   HIP_TRY(c, hipMemsetAsync(c->d_out, 0, (size_t)c->tile_w * c->tile_h * sizeof(float4), c->stream));
+  return CVR_OK;
+}
+
+int cvr_blocks_to_host(const float* device_src, float* host_dst, uint32_t width, uint32_t height, uint32_t rank,
+                       uint32_t world, float scale, void* stream) {
+  if (!device_src || !host_dst) return set_err(nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (width % 8 || height % 8 || world == 0 || rank >= world)
+    return set_err(nullptr, CVR_ERR_INVALID, "block shards need sides that are multiples of 8 and rank < world");
+  if ((((uintptr_t)device_src) | ((uintptr_t)host_dst)) & 15u)
+    return set_err(nullptr, CVR_ERR_INVALID, "image buffers must be 16-byte aligned");
+  if (width == 0 || height == 0) return CVR_OK;
+  void* dptr = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dptr, host_dst, 0);
+  if (e != hipSuccess || !dptr)
+    return set_err(nullptr, CVR_ERR_INVALID, "host buffer is not pinned or registered: %s", hipGetErrorString(e));
+  e = cvr::launch_blocks_to_host(device_src, static_cast<float*>(dptr), width, height, rank, world, scale,
+                                 static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return set_err(nullptr, CVR_ERR_HIP, "blocks_to_host: %s", hipGetErrorString(e));
   return CVR_OK;
 }
 
@@ -1388,7 +1436,9 @@ int cvr_trace_launch(cvr_ctx* c, cvr_path_record* out, uint64_t n_out) {
     return set_err(&c->err, CVR_ERR_INVALID, "record buffer holds %llu records, the launch range %llu",
                    (unsigned long long)n_out, (unsigned long long)count);
   const bool sparse = c->m.leaves != nullptr;
-  const uint64_t grid = c->grid_override ? c->grid_override : (uint64_t)(sparse ? c->wpool_grid_sparse : c->wpool_grid);
+  cvr::LaunchParams Lq{};
+  fill_launch(c, Lq, first, count);
+  const uint64_t grid = wpool_launch_grid(c, Lq.path_count);
   const size_t pid_bytes = (size_t)grid * cvr::wpool_slots(wpool_waves_for(c, sparse), sparse) * sizeof(uint32_t);
   const size_t rec_bytes = (size_t)count * sizeof(cvr_path_record);
   // the traced launch splats into a scratch framebuffer, not the context's

@@ -77,6 +77,8 @@ hipError_t launch_mk_init(const MediumParams& m, const LaunchParams& L, uint32_t
 hipError_t launch_mk_extend(const MediumParams& m, const LaunchParams& L, uint32_t iteration, uint32_t depth,
                             float4* st, uint32_t* live, MkCtl* ctl, hipStream_t s);
 hipError_t launch_image_to_host(const float* src, float* dst, size_t n, float scale, hipStream_t s);
+hipError_t launch_blocks_to_host(const float* src, float* dst, uint32_t w, uint32_t h, uint32_t rank, uint32_t world,
+                                 float scale, hipStream_t s);
 hipError_t launch_build_bounds(const float* density, uint32_t rx, uint32_t ry, uint32_t rz, uint32_t bshift,
                                float max_density, uint8_t* bounds, hipStream_t s);
 // Sparse medium: cell-leaf pool (`coords`: 3 u32 leaf coordinates per slot,

@@ -373,6 +373,38 @@ hipError_t launch_image_to_host(const float* src, float* dst, size_t n, float sc
   return hipGetLastError();
 }
 
+// The pixels of one block shard (cvr_set_block_shard(rank, world): 8x8 blocks
+// rank, rank + world, ..., row-major) normalised into the host image, at their
+// places in the full image: a multi-GPU render's whole output step, since the
+// ranks' block shards are pixel-disjoint (no reduction).  Four blocks per
+// workgroup, one pixel per work-item; eight work-items store one 128-byte row.
+__global__ __launch_bounds__(256) void k_blocks_to_host(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                        uint32_t w, uint32_t blocks_x, uint32_t n_mine, uint32_t rank,
+                                                        uint32_t world, float scale) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6); k < n_mine; k += gridDim.x * 4u) {
+    const uint32_t b = rank + k * world;
+    const uint32_t by = b / blocks_x, bx = b - by * blocks_x;
+    const size_t i = (size_t)(by * 8u + (lane >> 3)) * w + bx * 8u + (lane & 7u);
+    const float4 v = src[i];
+    __builtin_nontemporal_store(v.x / scale, &dst[i].x);
+    __builtin_nontemporal_store(v.y / scale, &dst[i].y);
+    __builtin_nontemporal_store(v.z / scale, &dst[i].z);
+    __builtin_nontemporal_store(v.w / scale, &dst[i].w);
+  }
+}
+
+hipError_t launch_blocks_to_host(const float* src, float* dst, uint32_t w, uint32_t h, uint32_t rank, uint32_t world,
+                                 float scale, hipStream_t s) {
+  const uint32_t blocks_x = w / 8u, n_blocks = blocks_x * (h / 8u);
+  const uint32_t n_mine = n_blocks > rank ? (n_blocks - rank + world - 1u) / world : 0u;
+  if (n_mine == 0u) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>((n_mine + 3u) / 4u, 1024u);
+  hipLaunchKernelGGL(k_blocks_to_host, dim3(grid), dim3(256), 0, s, reinterpret_cast<const float4*>(src),
+                     reinterpret_cast<float4*>(dst), w, blocks_x, n_mine, rank, world, scale);
+  return hipGetLastError();
+}
+
 // ----------------------------------------------------------- cell table ---
 // Corner-replicated density cells (see MediumParams::cells).
 __global__ __launch_bounds__(256) void k_build_cells(const float* __restrict__ D, uint32_t rx, uint32_t ry,

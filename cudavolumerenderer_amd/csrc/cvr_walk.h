@@ -190,11 +190,14 @@ struct LaunchParams {
   // grid * slots entries sits just below rec.  Null in production.
   void* rec;
   uint32_t chunk;         // paths per wave dequeue
-  uint32_t ev_thresh;     // persistent kernel: event batch threshold (lanes)
-  uint32_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track
+  uint16_t ev_thresh;     // persistent kernel: event batch threshold (lanes, <= 64)
+  uint16_t tail;          // pool kernel: a wave leaves TRACK when the pool is dry and fewer lanes track
   uint32_t batch;         // wave-pool kernel: idle lanes that trigger a swap
   uint32_t naive_mk;      // bit 0: trace kernel runs naiveMK paths (walk_mk) instead of path_begin + loop;
                           // bit 1: pool kernel sorts each track phase's paths by Morton code (streamingSK)
+  // Wave pool, once the queues are empty (the launch's drain): an event batch runs when
+  // waiting x drain >= tracking paths (0: only when no lane tracks or 64 events wait).
+  uint32_t drain;
   // Work order (scheduling only; results are bound to path ids).  order 0:
   // path ids in sample-major order from one queue.  order 1: 8x8-pixel
   // blocks with all their samples back to back (path_first must be a

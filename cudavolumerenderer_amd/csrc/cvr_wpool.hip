@@ -85,7 +85,8 @@ struct PoolSize {
 #ifdef CVR_WPOOL_SLOTS  // experiment builds: a smaller pool
   static constexpr int value = CVR_WPOOL_SLOTS;
 #else
-  static constexpr int value = (kBudget - kParams - 16 - 4 * STAT_COUNT) / (kSplit ? 64 : 80);
+  static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT) / (kSplit ? 64 : 80);
+  static_assert(4 * STAT_COUNT + 8 + 12 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
 #endif
 };
 // Sparse media (C5) keep the event part in LDS too: their cell-leaf pool
@@ -108,7 +109,7 @@ template <int kSlots, bool kSplit>
 struct WavePool {
   float4 a[kSlots], b[kSlots];
   uint4 c[kSlots];
-  float4 f[kSplit ? 1 : kSlots];  // (T, image_id) when not split
+  float4 f[kSplit ? 0 : kSlots];  // (T, image_id) when not split (none when split)
   uint2 e[kSlots];
   uint32_t meta[kSlots];
   uint8_t ready[kSlots];   // ring of track-ready slots
@@ -116,7 +117,13 @@ struct WavePool {
   uint8_t lc[kSlots];      // stack of real collisions
   uint8_t ln[kSlots];      // stack of slots waiting for a new path
   uint32_t cnt[STAT_COUNT];  // the wave's event counters (lane 0 adds per batch)
+  unsigned long long dead;   // queues this wave found empty (lane 0's dequeue skips them)
+  // the wave's path cursor into the global work queues: next, end, q | home << 8 | exhausted << 16
+  // (LDS, not SGPRs: only the regeneration code reads it, and the kernel has no scalar
+  // registers to spare)
+  uint32_t cur[3];
 };
+constexpr uint32_t kCurExhausted = 1u << 16;
 
 __device__ __forceinline__ uint32_t lane_rank(unsigned long long mask) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
@@ -206,10 +213,17 @@ __device__ __forceinline__ void record_end(const LaunchParams& L, uint32_t s, co
   static_cast<PathRecord*>(L.rec)[pid - L.path_first] = r;
 }
 
-struct Cursor {
-  uint32_t next, end, q, home;
-  bool exhausted;
-};
+
+// The launch parameters as seen from code that runs rarely (the drain): the
+// LDS address goes through an empty asm each time, so the compiler cannot
+// hoist loads of L's fields out of the main loop and hold them in registers
+// across the track loop (the dense kernel has no VGPR to spare at 5 waves).
+typedef __attribute__((address_space(3))) const LaunchParams LdsParams;
+__device__ __forceinline__ const LaunchParams& fresh(const LaunchParams& L) {
+  LdsParams* p = (LdsParams*)&L;
+  asm volatile("" : "+v"(p));
+  return *(const LaunchParams*)p;
+}
 
 }  // namespace
 
@@ -243,13 +257,16 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   // across the track loop); the track loop counts steps and fetches per lane.
   uint32_t c_steps = 0, c_fetch = 0;
   if (lane < (uint32_t)STAT_COUNT) S.cnt[lane] = 0u;
+  if (lane == 0) S.dead = 0ull;
   uint32_t n_over = 0;  // wave-uniform: segments whose last Woodcock step passed max_t
   // home queue: the XCD's band, and within it sub-queue (workgroup / 8) mod sub
   // (workgroups are dealt round-robin over the 8 XCDs)
-  Cursor cur{0, 0, 0,
-             ((__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % (L.n_queues / L.sub)) * L.sub +
-                 (blockIdx.x >> 3) % L.sub,
-             false};
+  if (lane == 0) {
+    S.cur[0] = S.cur[1] = 0u;
+    S.cur[2] = (((__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % (L.n_queues / L.sub)) * L.sub +
+                (blockIdx.x >> 3) % L.sub)
+               << 8;
+  }
   const uint32_t batch = L.batch;  // TRACK: swap finished segments once this many lanes are idle
   // wave-uniform list state
   uint32_t ready_head = 0, n_ready = 0, n_lb = 0, n_lc = 0;
@@ -326,7 +343,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0));
       // EVENT next: a full wave of waiting events, slots never filled, or
       // nothing left to track.  Park: tracking lanes return (t, rng) to the
-      // pool, finished lanes are filed.
+      // pool, finished lanes are filed.  (Once the queues are empty n_ln is a
+      // stand-in that lowers this threshold: see the end of the event batch.)
       if (n_lb + n_lc + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
         if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
         const unsigned long long mr = __ballot(slot >= 0 && fst == 0);
@@ -379,13 +397,13 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     }
 #endif
     // no path left (new-path slots only count while the queues have paths)
-    if (n_lb + n_lc == 0u && n_ready == 0u && (n_ln == 0u || cur.exhausted)) break;
+    if (n_lb + n_lc == 0u && n_ready == 0u && (n_ln == 0u || (S.cur[2] & kCurExhausted))) break;
 
     // ================================================= EVENT ==============
     __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
 #if CVR_TAILSTAMPS
     ++ts_n_ev;
-    if (cur.exhausted) ts_bstart = __builtin_amdgcn_s_memrealtime();
+    if (S.cur[2] & kCurExhausted) ts_bstart = __builtin_amdgcn_s_memrealtime();
 #endif
     // Event-code view of the medium: its BSDF / box / albedo fields pass
     // through opaque_s per batch, so values derived from them (HG and box
@@ -464,8 +482,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       n_lb -= tb;
       n_lc -= tc;
       n_ln -= tn;
-      PathState ps;
-      Isect is;
+      // zero-initialised: left undefined on the lanes that skip the event code,
+      // their values merge into loop-carried phis and the dense kernel spills
+      PathState ps{};
+      Isect is{};
       uint32_t nseg = 0;
       float t_hit = 0.0f;
       bool to_ready = false, to_lb = false, to_ln = false;
@@ -479,48 +499,62 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         const uint32_t rank = lane_rank(want);
         bool got = false;
         uint32_t given = 0;  // new items [0, given) get a path
-        while (given < (uint32_t)__popcll(want) && !cur.exhausted) {
-          if (cur.next == cur.end) {
+        uint32_t cnext = __builtin_amdgcn_readfirstlane(S.cur[0]), cend = __builtin_amdgcn_readfirstlane(S.cur[1]);
+        uint32_t cqh = __builtin_amdgcn_readfirstlane(S.cur[2]);
+        while (given < (uint32_t)__popcll(want) && !(cqh & kCurExhausted)) {
+          if (cnext == cend) {
+            // A queue found empty is never asked again (S.dead): once the
+            // queues run dry one after another, a wave would otherwise walk
+            // every empty head, one memory round trip each, per dequeue.
             uint32_t b = 0xFFFFFFFFu, qsel = 0;
             if (lane == 0) {
+              unsigned long long dead = S.dead;
               for (uint32_t k = 0; k < L.n_queues; ++k) {
-                const uint32_t q = (cur.home + k) % L.n_queues;
+                const uint32_t q = ((cqh >> 8) + k) % L.n_queues;
+                if ((dead >> q) & 1ull) continue;
                 const uint32_t g = atomicAdd(L.queue + 16 * q, L.chunk);
                 if (g < queue_units(L, q)) {
                   b = g;
                   qsel = q;
                   break;
                 }
+                dead |= 1ull << q;
               }
+              S.dead = dead;
             }
             b = __shfl(b, 0);
             qsel = __shfl(qsel, 0);
             if (b == 0xFFFFFFFFu) {
-              cur.exhausted = true;
+              cqh |= kCurExhausted;
 #if CVR_TAILSTAMPS
               ts_ex = __builtin_amdgcn_s_memrealtime();
               ts_steps_ex = c_steps;
 #endif
               break;
             }
-            cur.q = cur.home = qsel;
-            cur.next = b;
-            cur.end = min(b + L.chunk, queue_units(L, qsel));
+            cqh = qsel | qsel << 8;
+            cnext = b;
+            cend = min(b + L.chunk, queue_units(L, qsel));
           }
-          const uint32_t take = min((uint32_t)__popcll(want) - given, cur.end - cur.next);
+          const uint32_t take = min((uint32_t)__popcll(want) - given, cend - cnext);
           if (kind == K_NEW && rank >= given && rank < given + take) {
-            const uint32_t pid = unit_to_path(L, cur.q, cur.next + (rank - given));
+            const uint32_t pid = unit_to_path(L, cqh & 0xFFu, cnext + (rank - given));
             path_begin(L, pid, ps);
             if (kRecord) rec_pids<kSlots>(L)[s] = pid;
             is.normal = mk3(0, 0, 0);
             nseg = 0;
             got = true;
           }
-          cur.next += take;
+          cnext += take;
           given += take;
         }
+        if (lane == 0) {
+          S.cur[0] = cnext;
+          S.cur[1] = cend;
+          S.cur[2] = cqh;
+        }
         // first segment: AABB test (NaiveVolPTsk_kernel.cuh:33-47); a new item
-        // that got no path (queues exhausted) leaves its slot empty
+        // that got no path (queues exhausted) files its slot as free again
         const uint32_t n_got = (uint32_t)__popcll(__ballot(got));
         if (lane == 0) S.cnt[STAT_PATHS] += n_got;
         if (got) {
@@ -618,6 +652,22 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       n_ready += (uint32_t)__popcll(mr);
       n_lb += (uint32_t)__popcll(mb);
       n_ln += (uint32_t)__popcll(mn);
+    }
+    if (S.cur[2] & kCurExhausted) {
+      const uint32_t n_live = n_ready + n_lb + n_lc;
+      // The launch's drain.  A wave's lanes cannot all be busy any more, and
+      // a batch that waits for its slowest segment stretches the last paths'
+      // lives: the batch should run once drain x waiting >= tracking paths.
+      // n_ln (the new-path slots, which the empty queues cannot serve) stands
+      // in for that rule at no register cost in the track loop: with no path
+      // dying in between, tracking = n_live - waiting, so the event trigger
+      // waiting + n_ln >= 64 holds exactly when waiting >= n_live d / (d + 1).
+      // The batch's new items then get no path and run no code; their slot
+      // indices (the stack's stale entries) are never used.
+      {
+        const uint32_t d = fresh(L).drain;
+        n_ln = d ? 64u - min(64u, (n_live * d + d) / (d + 1u)) : 0u;
+      }
     }
 #if CVR_STAMPS
     {

@@ -30,8 +30,10 @@ Block shards (cvr_set_block_shard; bench.py's default strong-scaling mode):
 rank r renders the 8x8 pixel blocks r, r+world, ... of the tile with all
 their samples, so every rank keeps the pixel-block work order of the single-
 GPU kernel and sees the whole image (balanced whatever the scene); the ranks'
-path-id sets partition the launch (block_shard_path_ids), and one
-reduce-scatter sums the partial images.
+path-id sets partition the launch (block_shard_path_ids).  Their pixels are
+disjoint too, so there is nothing to reduce: each rank normalises its own
+blocks straight into the node's shared pinned host image (blocks_to_host,
+cvr_blocks_to_host), and the data path has no collective at all.
 """
 from __future__ import annotations
 
@@ -207,6 +209,44 @@ class HostImage:
                     os.unlink(self.path)
                 except OSError:
                     pass
+
+
+def block_pixel_index(width: int, height: int, rank: int, world: int):
+    """Flat pixel indices of block shard (rank, world) of a width x height
+    image (8x8 blocks rank, rank + world, ..., row-major), block by block,
+    each block's 64 pixels row-major: k_blocks_to_host's store order."""
+    import numpy as np
+    if width % 8 or height % 8:
+        raise ValueError("block shards need sides that are multiples of 8")
+    bx = width // 8
+    blocks = np.arange(rank, bx * (height // 8), world)
+    lane = np.arange(64)
+    px = (blocks[:, None] % bx) * 8 + (lane[None, :] & 7)
+    py = (blocks[:, None] // bx) * 8 + (lane[None, :] >> 3)
+    return (py * width + px).reshape(-1)
+
+
+def blocks_to_host(acc_flat, host: "HostImage", width: int, height: int, scale: float):
+    """The end of one block-sharded render on this rank: its pixels (the
+    blocks of shard (host.rank, host.world)) / scale into their places in the
+    shared host image.  No reduction: the ranks' blocks are disjoint.  On the
+    GPU one kernel on the current stream stores into the pinned / registered
+    image (cvr_blocks_to_host); host tensors (the gloo CPU tests) are indexed."""
+    n = width * height * 4
+    if acc_flat.is_cuda and host.pinned:
+        import torch
+        from . import _lib
+        _lib.blocks_to_host(acc_flat.data_ptr(), host.flat.data_ptr(), width, height, host.rank, host.world,
+                            float(scale), torch.cuda.current_stream().cuda_stream)
+        return
+    import torch
+    idx = torch.from_numpy(block_pixel_index(width, height, host.rank, host.world))
+    src = acc_flat[:n].view(-1, 4)
+    if src.is_cuda:
+        src = src[idx.to(src.device)].cpu()
+    else:
+        src = src[idx]
+    host.flat[:n].view(-1, 4)[idx] = src / scale
 
 
 KERNEL_COPY_MAX_BYTES = int(os.environ.get("CVR_KERNEL_COPY_MAX_BYTES", 4 << 20))

@@ -101,6 +101,15 @@ typedef enum {
   CVR_OPT_SUBQUEUES = 20,      /* wave-pool scheduler: work queues per XCD band (1..8, default 8), each
                                  over a contiguous part of the band, so that small dequeue chunks do not
                                  contend on one head.  Scheduling only. */
+  CVR_OPT_INFLIGHT = 23,       /* wave-pool scheduler: renders the caller keeps in flight on this device
+                                 (default 1).  Sets the grid of small launches (CVR_OPT_GRID 0): below 64
+                                 paths per wave of the occupancy grid half of it (a quarter with renders
+                                 in flight), below 1024 paths per wave half of it with renders in flight,
+                                 else all of it.  Scheduling only. */
+  /* 21: unused (a drain-time path migration between waves, measured slower: DESIGN.md §6) */
+  CVR_OPT_DRAIN = 22,          /* wave-pool scheduler, once the queues are empty: an event batch runs as
+                                 soon as the waiting segments x d >= the tracking ones (d = 0: only when
+                                 no lane tracks, or 64 events wait).  -1 (default) = 1.  Scheduling only. */
   CVR_OPT_MK_COMPACTION = 19   /* quirk Q11, naiveMK only: 0 (default) every live path is extended
                                  until it ends; 1 the reference's compaction count end - begin - 1
                                  (RenderKernelLauncher.cu:266-271): after every bounce the live path
@@ -261,6 +270,16 @@ int cvr_copy_output(cvr_ctx* ctx, float* host_rgba, float scale);
  * host memory: the transfer delegate's Scale + D->H copy
  * (ImageBufferTransfer.cu:61-78) in stream order, with no copy engine. */
 int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats, float scale, void* stream);
+/* Extension (multi-GPU output): the pixels of block shard (rank, world) of a
+ * width x height float4 image (cvr_set_block_shard: 8x8 blocks rank,
+ * rank + world, ..., row-major; sides multiples of 8), divided by `scale`,
+ * stored by a kernel on `stream` at their places in the full pinned or
+ * registered host image `host_dst` (width * height * 4 floats).  The ranks'
+ * block shards are pixel-disjoint, so every rank writing its own blocks into
+ * one shared host image IS the reference's Scale + D->H copy
+ * (ImageBufferTransfer.cu:61-78) of the whole render: no reduction. */
+int cvr_blocks_to_host(const float* device_src, float* host_dst, uint32_t width, uint32_t height, uint32_t rank,
+                       uint32_t world, float scale, void* stream);
 /* Debug/parity: trace path ids [first, first+count) one per work-item and
  * return per-path records (no framebuffer splat). */
 int cvr_trace_paths(cvr_ctx* ctx, uint32_t first, uint32_t count, cvr_path_record* host_out);

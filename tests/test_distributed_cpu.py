@@ -241,8 +241,9 @@ def test_block_shards_partition_path_ids(tw, th, samples, world):
         block_shard_path_ids(12, 8, 1, 0, 2)
 
 
-def _block_worker(rank, world, port, outdir):
-    from cudavolumerenderer_amd.distributed import HostImage, block_shard_path_ids, init_process_group, reduce_to_host
+def _block_worker(rank, world, port, outdir, mode):
+    from cudavolumerenderer_amd.distributed import (HostImage, block_shard_path_ids, blocks_to_host,
+                                                    init_process_group, reduce_to_host)
     # bench.py's process-group init (env rendezvous, as under torch.distributed.run)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     init_process_group(dist, "gloo")
@@ -260,8 +261,11 @@ def _block_worker(rank, world, port, outdir):
             esc = rec[(rec["flags"] & 1) != 0]
             np.add.at(acc[:, :3], esc["image_id"], esc["T"])
             acc[esc["image_id"], 3] = 1.0
-        part = torch.empty(host.chunk, dtype=torch.float32)
-        reduce_to_host(acc_flat, part, host, float(ITERS), dist)  # bench.py's end of a render
+        if mode == "blocks":  # bench.py's end of a block-sharded render: own blocks, no reduction
+            blocks_to_host(acc_flat, host, W, H, float(ITERS))
+        else:  # the reduce-scatter form (weak / tile modes)
+            part = torch.empty(host.chunk, dtype=torch.float32)
+            reduce_to_host(acc_flat, part, host, float(ITERS), dist)
         counts = torch.tensor([steps, len(ids)], dtype=torch.int64)
         dist.all_reduce(counts)
         dist.barrier()
@@ -273,13 +277,14 @@ def _block_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_block_shard_gloo_render_equals_single(tmp_path, world):
+@pytest.mark.parametrize("world,mode", [(2, "blocks"), (3, "blocks"), (2, "reduce"), (3, "reduce")])
+def test_block_shard_gloo_render_equals_single(tmp_path, world, mode):
     """bench.py's default multi-GPU step on CPU: every rank renders its block
-    shard (the oracle stands in for k_wpool), one reduce-scatter sums the
-    framebuffers, every rank normalises and writes its slice into the shared
-    host image; the image equals the 1-rank render /iterations."""
-    mp.start_processes(_block_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    shard (the oracle stands in for k_wpool) and writes its own blocks,
+    normalised, into the shared host image (blocks); or one reduce-scatter sums
+    the framebuffers and every rank writes its slice (reduce).  The image
+    equals the 1-rank render /iterations."""
+    mp.start_processes(_block_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True,
                        start_method="fork")
     img = np.load(tmp_path / "img.npy")
     counts = np.load(tmp_path / "counts.npy")

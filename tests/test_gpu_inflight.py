@@ -205,6 +205,42 @@ def test_image_to_host_matches_division(cvr):
             hip.hipHostFree(h_buf)
 
 
+@pytest.mark.parametrize("w,h,world", [(64, 48, 1), (64, 48, 3), (1024, 1024, 8), (24, 8, 5)])
+def test_blocks_to_host_writes_own_blocks(cvr, w, h, world):
+    """cvr_blocks_to_host: every rank's kernel stores exactly its block
+    shard's pixels (distributed.block_pixel_index), x / scale bit for bit,
+    and leaves the other pixels alone; the world's ranks together fill the
+    image (the multi-GPU output step without a reduction)."""
+    import ctypes as C
+    from cudavolumerenderer_amd.distributed import block_pixel_index
+    hip = C.CDLL("libamdhip64.so.7")
+    P = C.c_void_p
+    n = w * h * 4
+    a = (np.random.default_rng(w + world).standard_normal(n) * 1e3).astype(np.float32)
+    d_src, h_buf = P(), P()
+    assert hip.hipMalloc(C.byref(d_src), C.c_size_t(n * 4)) == 0
+    assert hip.hipHostMalloc(C.byref(h_buf), C.c_size_t(n * 4), 0) == 0
+    try:
+        assert hip.hipMemcpy(d_src, a.ctypes.data_as(P), C.c_size_t(n * 4), 1) == 0  # H2D
+        host = np.ctypeslib.as_array(C.cast(h_buf, C.POINTER(C.c_float)), shape=(n,))
+        host[:] = np.nan
+        want = np.full(n, np.nan, np.float32).reshape(-1, 4)
+        for r in range(world):
+            cvr._lib.blocks_to_host(d_src.value, h_buf.value, w, h, r, world, 20.0, None)
+            assert hip.hipDeviceSynchronize() == 0
+            idx = block_pixel_index(w, h, r, world)
+            want[idx] = a.reshape(-1, 4)[idx] / np.float32(20.0)
+            got = host.reshape(-1, 4)
+            assert np.array_equal(np.isnan(got), np.isnan(want)), f"rank {r}: wrong pixels written"
+            assert np.array_equal(got[idx], want[idx]), f"rank {r}"
+        assert not np.isnan(host).any()
+        with pytest.raises(cvr.CvrError):
+            cvr._lib.blocks_to_host(d_src.value, h_buf.value, w + 4, h, 0, world, 1.0, None)
+    finally:
+        hip.hipFree(d_src)
+        hip.hipHostFree(h_buf)
+
+
 def test_shared_sparse_medium_in_flight(cvr):
     """A small sparse cloud (leaves, cell-leaf pool, brick words) shared by a
     second context on its own stream: both launched back to back without a

@@ -84,6 +84,8 @@ def main():
             c.set_option(cvr.OPT_QUEUES, d["queues"])
         if "sub" in d:
             c.set_option(cvr.OPT_SUBQUEUES, d["sub"])
+        if "drain" in d:
+            c.set_option(cvr.OPT_DRAIN, d["drain"])
         if "waves" in d:
             c.set_option(cvr.OPT_WAVES, d["waves"])
         if "batch" in d:
