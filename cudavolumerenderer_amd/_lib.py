@@ -121,6 +121,7 @@ def load() -> C.CDLL:
         "cvr_share_medium": (I32, [P, P]),
         "cvr_trace_launch": (I32, [P, P, U64]),
         "cvr_image_to_host": (I32, [P, P, C.c_size_t, C.c_float, P]),
+        "cvr_render_frame": (I32, [P, P, U32, C.POINTER(Stats)]),
         "cvr_blocks_to_host": (I32, [P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float, P]),
         "cvr_launch_blocks": (I32, [P, P, P, P]),
         "cvr_set_seed": (I32, [P, U32]),
@@ -383,6 +384,7 @@ class Context:
 
     def set_resolution(self, w, h):
         self._c(load().cvr_set_resolution(self._h, w, h))
+        self.resolution = (w, h)
 
     def set_offset(self, x, y):
         self._c(load().cvr_set_offset(self._h, x, y))
@@ -487,6 +489,21 @@ class Context:
     def render_image(self, width, height, n_tiles=(1, 1), iterations=20, device_image: Optional[int] = None,
                      host: bool = True):
         return self.render_tiles(width, height, n_tiles, iterations, 0, 1, device_image, host)
+
+    def render_frame(self, host_ptr: Optional[int] = None, parts: int = 0):
+        """CudaVolPath::render for one tile (cvr_render_frame): clear, render
+        the set resolution / iterations, and the normalised image in host
+        memory when it returns, the launch split into `parts` bands whose
+        copies overlap the later bands.  host_ptr: a width*height*4 float
+        buffer (pinned for asynchronous copies); None returns a new array."""
+        st = Stats()
+        img = None
+        if host_ptr is None:
+            w, h = self.resolution
+            img = np.zeros((h, w, 4), np.float32)
+            host_ptr = img.ctypes.data
+        self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), parts, C.byref(st)))
+        return img, st
 
     def render_tiles(self, width, height, n_tiles=(1, 1), iterations=20, first_tile: int = 0,
                      tile_stride: int = 1, device_image: Optional[int] = None, host: bool = True):

@@ -158,6 +158,17 @@ struct cvr_ctx {
   bool wf_timing = false;
 
   cvr_stats last{};
+
+  // cvr_render_frame: this launch's band of block rows (band_count 0: every block), the
+  // helper contexts that render the frame's other bands (each with its own stream and work
+  // queues, sharing this context's medium and framebuffer), the copy stream, and the
+  // normalised device image the bands are copied from
+  uint32_t band_first = 0, band_count = 0;
+  std::vector<cvr_ctx*> frame_kids;
+  hipStream_t frame_copy = nullptr;
+  hipEvent_t frame_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] cleared, [1 + k] band k rendered
+  float4* d_frame = nullptr;
+  size_t frame_px = 0;
 };
 
 #ifndef CVR_TAILSTAMPS
@@ -319,6 +330,10 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
       L.blk_off = c->shard_rank;
       L.blk_stride = c->shard_world;
       L.n_blocks = L.n_blocks > c->shard_rank ? (L.n_blocks - c->shard_rank + c->shard_world - 1) / c->shard_world : 0;
+      L.path_count = L.n_blocks * 64u * L.samples;
+    } else if (c->band_count && block_order && c->band_first < L.n_blocks) {  // cvr_render_frame's band
+      L.blk_off = c->band_first;
+      L.n_blocks = std::min(c->band_count, L.n_blocks - c->band_first);
       L.path_count = L.n_blocks * 64u * L.samples;
     }
     uint32_t bands = c->n_queues < L.n_blocks ? c->n_queues : L.n_blocks;
@@ -615,6 +630,10 @@ static void free_sparse(cvr_ctx* c);
 int cvr_destroy(cvr_ctx* c) {
   if (!c) return CVR_OK;
   (void)hipSetDevice(c->device);
+  // the frame helpers first: their launches read this context's medium and framebuffer
+  for (cvr_ctx* k : c->frame_kids) cvr_destroy(k);
+  c->frame_kids.clear();
+  if (c->frame_copy) (void)hipStreamSynchronize(c->frame_copy);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->d_density) (void)hipFree(c->d_density);
   if (c->d_albedo) (void)hipFree(c->d_albedo);
@@ -632,6 +651,10 @@ int cvr_destroy(cvr_ctx* c) {
   if (c->d_pool) (void)hipFree(c->d_pool);
   if (c->h_alive) (void)hipHostFree(c->h_alive);
   for (auto& e : c->it_events) (void)hipEventDestroy(e);
+  for (auto& e : c->frame_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->frame_copy) (void)hipStreamDestroy(c->frame_copy);
+  if (c->d_frame) (void)hipFree(c->d_frame);
   delete c;
   return CVR_OK;
 }
@@ -1571,6 +1594,158 @@ done:
     (void)hipFree(tmp_img);
   }
   return r;
+}
+
+// The launcher settings a helper context of cvr_render_frame takes from its
+// parent: everything but its own resources (stream, work queues, scratch).
+static void copy_settings(cvr_ctx* d, const cvr_ctx* s) {
+  d->m = s->m;  // the parent's medium (re-shared every frame: the parent may have loaded another)
+  d->n_cell_leaves = s->n_cell_leaves;
+  d->have_medium = s->have_medium;
+  memcpy(d->inv_view, s->inv_view, sizeof(d->inv_view));
+  d->r2v[0] = s->r2v[0];
+  d->r2v[1] = s->r2v[1];
+  d->full_res[0] = s->full_res[0];
+  d->full_res[1] = s->full_res[1];
+  d->have_camera = s->have_camera;
+  d->tile_w = s->tile_w;
+  d->tile_h = s->tile_h;
+  d->off[0] = s->off[0];
+  d->off[1] = s->off[1];
+  d->iterations = s->iterations;
+  d->n_paths = s->n_paths;
+  d->range_first = s->range_first;
+  d->range_count = s->range_count;
+  d->shard_rank = s->shard_rank;
+  d->shard_world = s->shard_world;
+  d->seed = s->seed;
+  d->n_queues = s->n_queues;
+  d->subqueues = s->subqueues;
+  d->drain = s->drain;
+  d->order = s->order;
+  d->max_segments = s->max_segments;
+  d->chunk = s->chunk;
+  d->ev_thresh = s->ev_thresh;
+  d->grid_override = s->grid_override;
+  d->inflight = s->inflight;
+  d->scatter_eps = s->scatter_eps;
+  d->rng_binding = s->rng_binding;
+  d->world_to_aabb = s->world_to_aabb;
+  d->mk_compaction = s->mk_compaction;
+  d->pool_tail = s->pool_tail;
+  d->wpool_waves = s->wpool_waves;
+  d->morton = s->morton;
+  d->swap_batch = s->swap_batch;
+  d->scheduler = s->scheduler;
+  d->waves = s->waves;
+  d->pool_max = s->pool_max;
+}
+
+int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* stats) {
+  if (!c || !host_image) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  int r = check_ready(c);
+  if (r) return r;
+  if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
+  if ((r = do_init(c))) return r;
+  const uint32_t W = c->tile_w, H = c->tile_h;
+  const size_t px = (size_t)W * H;
+  // bands need the pixel-block work order of a whole-sample, unsharded, queued launch
+  uint64_t first, count;
+  compute_range(c, &first, &count);
+  cvr::LaunchParams L0{};
+  fill_launch(c, L0, first, count);
+  const bool queued = c->kernel != CVR_KERNEL_NAIVE_SK && c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 &&
+                      c->rng_binding == 0;
+  const uint32_t brows = (L0.order == 1 && queued && c->shard_world == 1) ? H / 8u : 0u;
+  if (parts == 0) parts = 1;
+  parts = std::min<uint32_t>(parts, 3u);
+  if (brows < parts) parts = brows ? brows : 1u;
+  // band k takes (parts - k) shares of the block rows: the last band, whose copy
+  // the frame waits for, is the smallest
+  uint32_t row0[4] = {0, 0, 0, 0};
+  {
+    const uint32_t shares = parts * (parts + 1) / 2;
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < parts; ++k) {
+      acc += parts - k;
+      row0[k + 1] = k + 1 == parts ? brows : (uint32_t)((uint64_t)brows * acc / shares);
+    }
+  }
+  while (c->frame_kids.size() + 1 < parts) {
+    cvr_ctx* k = nullptr;
+    if ((r = cvr_create(c->device, c->kernel, &k))) return set_err(&c->err, r, "frame helper: %s", g_last_error.c_str());
+    c->frame_kids.push_back(k);
+  }
+  if (!c->frame_copy) {
+    int lo = 0, hi = 0;
+    HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(c, hipStreamCreateWithPriority(&c->frame_copy, hipStreamNonBlocking, hi));
+    for (auto& e : c->frame_ev) HIP_TRY(c, hipEventCreate(&e));
+  }
+  if (c->frame_px < px) {
+    HIP_TRY(c, hipStreamSynchronize(c->frame_copy));
+    if (c->d_frame) (void)hipFree(c->d_frame);
+    c->d_frame = nullptr;
+    c->frame_px = 0;
+    HIP_TRY(c, hipMalloc(&c->d_frame, px * sizeof(float4)));
+    c->frame_px = px;
+  }
+  // clear (initRenderState), then every band on its own stream
+  HIP_TRY(c, hipMemsetAsync(c->d_out, 0, px * sizeof(float4), c->stream));
+  HIP_TRY(c, hipEventRecord(c->frame_ev[0], c->stream));
+  cvr_ctx* who[3] = {c, nullptr, nullptr};
+  for (uint32_t k = 1; k < parts; ++k) {
+    cvr_ctx* kid = c->frame_kids[k - 1];
+    copy_settings(kid, c);
+    kid->d_out = c->d_out;
+    kid->external_out = true;
+    if ((r = do_init(kid))) return set_err(&c->err, r, "frame helper: %s", kid->err.c_str());
+    HIP_TRY(c, hipStreamWaitEvent(kid->stream, c->frame_ev[0], 0));
+    who[k] = kid;
+  }
+  const float scale = (float)c->iterations;
+  for (uint32_t k = 0; k < parts; ++k) {
+    cvr_ctx* x = who[k];
+    x->band_first = brows ? row0[k] * (W / 8u) : 0u;
+    x->band_count = brows ? (row0[k + 1] - row0[k]) * (W / 8u) : 0u;
+    r = cvr_launch_render(x);
+    x->band_first = x->band_count = 0;
+    if (r) return x == c ? r : set_err(&c->err, r, "frame band %u: %s", k, x->err.c_str());
+    HIP_TRY(c, hipEventRecord(c->frame_ev[1 + k], x->stream));
+    // getImage of the band's rows (ImageBufferTransfer.cu:61-78: Scale, then the D->H
+    // copy) on the copy stream, while the later bands render
+    const uint32_t y0 = brows ? row0[k] * 8u : 0u, y1 = brows ? row0[k + 1] * 8u : H;
+    HIP_TRY(c, hipStreamWaitEvent(c->frame_copy, c->frame_ev[1 + k], 0));
+    HIP_TRY(c, cvr::launch_tile_to_image(c->d_out + (size_t)y0 * W, W, y1 - y0, c->d_frame, W, 0, y0, scale,
+                                         c->frame_copy));
+    HIP_TRY(c, hipMemcpyAsync(host_image + (size_t)y0 * W * 4, c->d_frame + (size_t)y0 * W,
+                              (size_t)(y1 - y0) * W * sizeof(float4), hipMemcpyDeviceToHost, c->frame_copy));
+  }
+  HIP_TRY(c, hipStreamSynchronize(c->frame_copy));
+  cvr_stats acc{};
+  for (uint32_t k = 0; k < parts; ++k) {
+    cvr_stats s{};
+    if ((r = cvr_get_stats(who[k], &s))) return who[k] == c ? r : set_err(&c->err, r, "%s", who[k]->err.c_str());
+    acc.paths += s.paths;
+    acc.segments += s.segments;
+    acc.steps += s.steps;
+    acc.density += s.density;
+    acc.albedo += s.albedo;
+    acc.escaped += s.escaped;
+    acc.truncated += s.truncated;
+    acc.fetches += s.fetches;
+  }
+  float ms = 0.f;  // clear to the end of the band that ends last
+  for (uint32_t k = 0; k < parts; ++k) {
+    float t = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&t, c->frame_ev[0], c->frame_ev[1 + k]));
+    ms = std::max(ms, t);
+  }
+  acc.kernel_ms = ms;
+  c->last = acc;
+  if (stats) *stats = acc;
+  c->seed = seed_after_resets(c, c->seed, 1);  // reset(): prepareForNextIterations
+  return CVR_OK;
 }
 
 // ------------------------------------------------------------- helpers ----

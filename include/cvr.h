@@ -270,6 +270,24 @@ int cvr_copy_output(cvr_ctx* ctx, float* host_rgba, float scale);
  * host memory: the transfer delegate's Scale + D->H copy
  * (ImageBufferTransfer.cu:61-78) in stream order, with no copy engine. */
 int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats, float scale, void* stream);
+/* CudaVolPath::render for one tile (CudaVolPath.cpp:339-347, getImage
+ * ImageBufferTransfer.cu:61-78): clear the framebuffer, render the context's
+ * launch (resolution, iterations, camera, offset as set) and return once the
+ * image, divided by the iteration count, is in `host_image` (width * height
+ * float4; pinned memory makes the copy asynchronous).  parts 0 or 1: one
+ * launch.  parts 2..3: the launch split into bands of 8-pixel block rows, the
+ * largest first, each rendered with its own stream and work queues (helper
+ * contexts that share this context's medium and framebuffer), so that a
+ * band's normalise + copy runs while the later bands render; measured slower
+ * on C2 (5.35 / 5.66 ms for 2 / 3 bands vs 5.37 for one launch: each band
+ * adds ~0.15 ms of kernel span, more than its overlapped copy saves;
+ * DESIGN.md §6).  Every path renders exactly as in one launch (the RNG is bound
+ * to the path id).  Launches that cannot take bands (naive kernels, the
+ * thread-bound RNG, sides that are not multiples of 8, partial path ranges,
+ * block shards) render as one part.  Afterwards the seed has advanced as the
+ * reference's reset() advances it (cvr_reset).  stats: the summed counters;
+ * kernel_ms = from the clear to the end of the last band. */
+int cvr_render_frame(cvr_ctx* ctx, float* host_image, uint32_t parts, cvr_stats* stats);
 /* Extension (multi-GPU output): the pixels of block shard (rank, world) of a
  * width x height float4 image (cvr_set_block_shard: 8x8 blocks rank,
  * rank + world, ..., row-major; sides multiples of 8), divided by `scale`,

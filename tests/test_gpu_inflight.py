@@ -270,3 +270,47 @@ def test_shared_sparse_medium_in_flight(cvr):
 def c_out(c):
     c.synchronize()
     return c.copy_output(W, H), c.stats()
+
+
+@pytest.mark.parametrize("kernel,parts,res", [("regenerationSK", 3, (256, 256)), ("regenerationSK", 2, (256, 200)),
+                                              ("sortingSK", 3, (256, 256)), ("regenerationSK", 1, (256, 256)),
+                                              ("regenerationSK", 3, (250, 256)), ("naiveSK", 3, (256, 256)),
+                                              ("regenerationSK", 3, (64, 16))])
+def test_render_frame_equals_render_image(cvr, kernel, parts, res):
+    """cvr_render_frame (one synchronous render, the launch split into bands
+    of block rows on helper contexts, each band's normalise + copy overlapping
+    the later bands) leaves the same image in host memory as render_image's
+    single launch, with the same counters; kernels and sizes that cannot take
+    bands (naiveSK, a side that is not a multiple of 8) render as one part.
+    Repeated calls reuse the helpers; a second medium loaded into the owner is
+    what the helpers render next."""
+    w, h = res
+    scene = cvr.Scene.synthetic("manix")
+    c = cvr.Context(0, kernel)
+    c.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(w, h)
+    c.set_camera(iv, r2v, (w, h))
+    c.init()
+    ref, rst = c.render_image(w, h, (1, 1), ITERS)
+    c.set_resolution(w, h)
+    c.set_iterations(ITERS)
+    for rep in range(2):
+        c.set_seed(0)  # render_image's tile 0 seed; both calls advance it as reset() does
+        img, st = c.render_frame(None, parts)
+        assert c.get_seed() == {"regenerationSK": w * h * ITERS, "sortingSK": 1}.get(kernel, 0)
+        for k in ("paths", "segments", "steps", "density", "albedo", "escaped", "fetches"):
+            assert getattr(st, k) == getattr(rst, k), (k, rep)
+        assert_pixels_close(img[..., :3], ref[..., :3], ITERS, f"render_frame {kernel} {parts} parts")
+        assert st.kernel_ms > 0
+    # another medium in the owner: the helpers follow it
+    other = cvr.Scene.synthetic("hetvol")
+    c.set_medium(other.medium)
+    c.set_seed(0)
+    ref2, rst2 = c.render_image(w, h, (1, 1), ITERS)
+    c.set_resolution(w, h)
+    c.set_iterations(ITERS)
+    c.set_seed(0)
+    img2, st2 = c.render_frame(None, parts)
+    assert st2.steps == rst2.steps and st2.escaped == rst2.escaped
+    assert_pixels_close(img2[..., :3], ref2[..., :3], ITERS, "render_frame after a new medium")
+    c.close()
