@@ -314,3 +314,41 @@ def test_render_frame_equals_render_image(cvr, kernel, parts, res):
     assert st2.steps == rst2.steps and st2.escaped == rst2.escaped
     assert_pixels_close(img2[..., :3], ref2[..., :3], ITERS, "render_frame after a new medium")
     c.close()
+
+
+def test_framebuffer_growth_keeps_work_order_tables(cvr):
+    """growing the owned framebuffer (cvr_set_resolution to a
+    larger tile after renders with the Morton work order and a block order)
+    must neither free nor reuse the work-order tables: the next render at the
+    new size equals a fresh context's, and destroying the context is clean."""
+    scene = cvr.Scene.synthetic("manix")
+    c = cvr.Context(0, "regenerationSK")
+    c.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(256, 256)
+    c.set_camera(iv, r2v, (256, 256))
+    c.init()
+    c.set_resolution(64, 64)
+    c.set_iterations(2)
+    c.clear_output()
+    c.launch_render()
+    c.synchronize()
+    nb, _, _ = c.launch_blocks()
+    c.set_block_order(np.arange(nb, dtype=np.uint32)[::-1].copy())
+    c.clear_output()
+    c.launch_render()
+    c.synchronize()
+    c.set_resolution(256, 256)  # the owned framebuffer grows
+    c.set_iterations(ITERS)
+    big, sb = _render(c)
+    f = cvr.Context(0, "regenerationSK")
+    f.share_medium(c)
+    f.set_camera(iv, r2v, (256, 256))
+    f.init()
+    f.set_resolution(256, 256)
+    f.set_iterations(ITERS)
+    ref, sr = _render(f)
+    for k in ("paths", "segments", "steps", "escaped", "fetches"):
+        assert getattr(sb, k) == getattr(sr, k), k
+    assert_pixels_close(big, ref, ITERS, "after framebuffer growth")
+    f.close()
+    c.close()
