@@ -4,7 +4,7 @@
 set -eu
 cd "$(dirname "$0")/.."
 F=gpurun_out/final
-P=${1:-profiles/round2}
+P=${1:-profiles/round3}
 for sc in manix hetvol cloud; do
   case $sc in manix) key=k_wpool_1024x1024_20it; c=c2;; hetvol) key=hetvol_k_wpool_1024x1024_20it; c=c3;;
                      cloud) key=cloud_k_wpool_4096x4096_20it; c=c5;; esac
@@ -13,7 +13,8 @@ for sc in manix hetvol cloud; do
   if [ $sc = cloud ]; then sw="3 1"; else sw="10 2"; fi
   python3 tools/kernel_phases.py $F/prof_$sc/run_kernel_trace.csv k_wpool $sw $P/${c}_kernel_phases.json | grep _ms
 done
-python3 tools/pmc_summary.py $P/pmc_k_wpool.json k_wpool $F/pmc_a $F/pmc_b $F/pmc_c
+python3 tools/pmc_summary.py $P/pmc_k_wpool.json k_wpool $F/pmc_a $F/pmc_b $F/pmc_c $F/pmc_d
+python3 tools/pmc_summary.py $P/pmc_k_wpool_cloud.json k_wpool $F/pmc5_a $F/pmc5_b $F/pmc5_c
 for c in c1 c2 c3 c4 c5; do
   cp $F/${c}_bench.log $P/${c}_bench.log
   grep '^{' $F/${c}_bench.log | python3 -c "
