@@ -15,6 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libcvr.so")
+_DEFAULT_LIB = os.path.abspath(LIB_PATH)
 
 CVR_OK = 0
 ERRORS = {-1: "CVR_ERR_INVALID", -2: "CVR_ERR_HIP", -3: "CVR_ERR_STATE", -4: "CVR_ERR_IO",
@@ -156,7 +157,12 @@ def load() -> C.CDLL:
         "cvr_kernel_from_name": (I32, [C.c_char_p]),
         "cvr_kernel_name": (C.c_char_p, [I32]),
     }
+    # an older experiment build (tools' --lib, A/B against a previous commit) may lack newer entry
+    # points; the in-tree library must export every one (tests/test_host_abi.py)
+    older_ok = os.path.abspath(LIB_PATH) != _DEFAULT_LIB
     for name, (res, args) in sig.items():
+        if older_ok and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
