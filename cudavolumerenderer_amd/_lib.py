@@ -496,19 +496,20 @@ class Context:
                      host: bool = True):
         return self.render_tiles(width, height, n_tiles, iterations, 0, 1, device_image, host)
 
-    def render_frame(self, host_ptr: Optional[int] = None, parts: int = 0):
+    def render_frame(self, host_ptr: Optional[int] = None, parts: int = 0, stats: bool = True):
         """CudaVolPath::render for one tile (cvr_render_frame): clear, render
         the set resolution / iterations, and the normalised image in host
         memory when it returns, the launch split into `parts` bands whose
         copies overlap the later bands.  host_ptr: a width*height*4 float
-        buffer (pinned for asynchronous copies); None returns a new array."""
-        st = Stats()
+        buffer (pinned for asynchronous copies); None returns a new array.
+        stats=False skips the counters (one synchronous read per band)."""
+        st = Stats() if stats else None
         img = None
         if host_ptr is None:
             w, h = self.resolution
             img = np.zeros((h, w, 4), np.float32)
             host_ptr = img.ctypes.data
-        self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), parts, C.byref(st)))
+        self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), parts, C.byref(st) if stats else None))
         return img, st
 
     def render_tiles(self, width, height, n_tiles=(1, 1), iterations=20, first_tile: int = 0,

@@ -1722,6 +1722,8 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* s
                               (size_t)(y1 - y0) * W * sizeof(float4), hipMemcpyDeviceToHost, c->frame_copy));
   }
   HIP_TRY(c, hipStreamSynchronize(c->frame_copy));
+  c->seed = seed_after_resets(c, c->seed, 1);  // reset(): prepareForNextIterations
+  if (!stats) return CVR_OK;  // the counters cost a synchronous read per band
   cvr_stats acc{};
   for (uint32_t k = 0; k < parts; ++k) {
     cvr_stats s{};
@@ -1743,8 +1745,7 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* s
   }
   acc.kernel_ms = ms;
   c->last = acc;
-  if (stats) *stats = acc;
-  c->seed = seed_after_resets(c, c->seed, 1);  // reset(): prepareForNextIterations
+  *stats = acc;
   return CVR_OK;
 }
 

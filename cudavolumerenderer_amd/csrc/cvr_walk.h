@@ -772,7 +772,11 @@ CVR_DEV bool roulette(PathState& ps) {
   return true;
 }
 // atomicVectorAdd (Utilities.cuh:15-22) with Le = 1.
+#ifndef CVR_DIAG_NO_SPLAT  // diagnostic builds only (tools/job_writes.sh): no framebuffer writes
+#define CVR_DIAG_NO_SPLAT 0
+#endif
 CVR_DEV void splat(const LaunchParams& L, const PathState& ps) {
+  if (CVR_DIAG_NO_SPLAT) return;
   float* px = reinterpret_cast<float*>(L.out + ps.image_id);
   atomicAdd(px + 0, ps.T.x);
   atomicAdd(px + 1, ps.T.y);

@@ -447,7 +447,18 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #define CVR_WPOOL_NEW_FORCE 64
 #endif
       uint32_t tb, tc, tn;
-      if (CVR_WPOOL_KIND_MIN > 0 && n_lb >= (uint32_t)CVR_WPOOL_KIND_MIN) {
+#ifndef CVR_WPOOL_MAJORITY  // experiment: every batch runs one kind, the one with more items waiting
+#define CVR_WPOOL_MAJORITY 0
+#endif
+      if (CVR_WPOOL_MAJORITY && n_lb + n_ln >= n_lc) {
+        tb = min(n_lb, 64u);
+        tc = 0;
+        tn = min(n_ln, 64u - tb);
+      } else if (CVR_WPOOL_MAJORITY) {
+        tb = 0;
+        tc = min(n_lc, 64u);
+        tn = 0;
+      } else if (CVR_WPOOL_KIND_MIN > 0 && n_lb >= (uint32_t)CVR_WPOOL_KIND_MIN) {
         tb = min(n_lb, 64u);
         tc = 0;
         tn = min(n_ln, 64u - tb);

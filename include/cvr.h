@@ -285,7 +285,8 @@ int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats,
  * to the path id).  Launches that cannot take bands (naive kernels, the
  * thread-bound RNG, sides that are not multiples of 8, partial path ranges,
  * block shards) render as one part.  Afterwards the seed has advanced as the
- * reference's reset() advances it (cvr_reset).  stats: the summed counters;
+ * reference's reset() advances it (cvr_reset).  stats (may be NULL, which
+ * saves a synchronous counter read per band): the summed counters;
  * kernel_ms = from the clear to the end of the last band. */
 int cvr_render_frame(cvr_ctx* ctx, float* host_image, uint32_t parts, cvr_stats* stats);
 /* Extension (multi-GPU output): the pixels of block shard (rank, world) of a
