@@ -450,7 +450,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #ifndef CVR_WPOOL_MAJORITY  // experiment: every batch runs one kind, the one with more items waiting
 #define CVR_WPOOL_MAJORITY 0
 #endif
-      if (CVR_WPOOL_MAJORITY && n_lb + n_ln >= n_lc) {
+      // (once the queues are empty n_ln is the drain rule's stand-in, not new paths)
+      if (CVR_WPOOL_MAJORITY && n_lb + ((S.cur[2] & kCurExhausted) ? 0u : n_ln) >= n_lc) {
         tb = min(n_lb, 64u);
         tc = 0;
         tn = min(n_ln, 64u - tb);
