@@ -1534,6 +1534,13 @@ int cvr_render_tiles(cvr_ctx* c, const cvr_render_desc* d, uint32_t first_tile, 
   if ((r = check_ready(c))) return r;
   const uint32_t W = d->resolution[0], H = d->resolution[1];
   const uint32_t ntiles = d->n_tiles[0] * d->n_tiles[1];
+  if (ntiles == 1 && first_tile == 0 && !device_image && host_image && !c->external_out) {
+    // one tile into host memory: cvr_render_frame (no scratch image per call; the same
+    // clear, launch, Scale + copy and seed advance as the loop below)
+    if ((r = cvr_set_offset(c, 0, 0))) return r;
+    if ((r = ensure_output(c))) return r;
+    return cvr_render_frame(c, host_image, 1, stats);
+  }
   float4* dimg = static_cast<float4*>(device_image);
   float4* tmp_img = nullptr;
   if (!dimg && host_image) {
