@@ -417,18 +417,29 @@ def test_wave_pool_scheduler_matches_persistent(cvr, scenes, scene_key):
     ref.set_option(cvr.OPT_SCHEDULER, 0)  # the per-wave persistent kernel
     img0, st0 = ref.render_image(W, H, (1, 1), 4)
     key0 = (st0.paths, st0.segments, st0.steps, st0.density, st0.albedo, st0.escaped, st0.fetches)
-    for batch, grid, chunk, order in [(8, 0, 256, 1), (1, 0, 64, 1), (64, 5, 256, 1), (16, 1, 7, 0),
-                                      (32, 3, 1, 1)]:
+    # + the drain-time event rule (CVR_OPT_DRAIN 0 / 1 / 3), the in-flight grid rule
+    # (CVR_OPT_INFLIGHT) and the sub-queues per XCD band (CVR_OPT_SUBQUEUES)
+    for batch, grid, chunk, order, drain, inflight, sub in [
+            (8, 0, 256, 1, 1, 1, 8), (1, 0, 64, 1, 0, 1, 8), (64, 5, 256, 1, 3, 1, 1), (16, 1, 7, 0, 1, 1, 8),
+            (32, 3, 1, 1, 0, 1, 3), (8, 0, None, 2, 1, 3, 8), (8, 0, None, 2, 2, 64, 2)]:
         ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
         ctx.set_option(cvr.OPT_SCHEDULER, 3)
         ctx.set_option(cvr.OPT_BATCH, batch)
         ctx.set_option(cvr.OPT_GRID, grid)
-        ctx.set_option(cvr.OPT_CHUNK, chunk)
+        if chunk is not None:  # None: the automatic chunk
+            ctx.set_option(cvr.OPT_CHUNK, chunk)
         ctx.set_option(cvr.OPT_ORDER, order)
+        ctx.set_option(cvr.OPT_DRAIN, drain)
+        ctx.set_option(cvr.OPT_INFLIGHT, inflight)
+        ctx.set_option(cvr.OPT_SUBQUEUES, sub)
         img, st = ctx.render_image(W, H, (1, 1), 4)
         key = (st.paths, st.segments, st.steps, st.density, st.albedo, st.escaped, st.fetches)
-        assert key == key0, (batch, grid, chunk, order)
+        assert key == key0, (batch, grid, chunk, order, drain, inflight, sub)
         assert_pixels_close(img, img0, 4)
+    with pytest.raises(cvr.CvrError):
+        ctx.set_option(cvr.OPT_DRAIN, 65)
+    with pytest.raises(cvr.CvrError):
+        ctx.set_option(cvr.OPT_INFLIGHT, 0)
 
 
 @pytest.mark.parametrize("kernel", ["regenerationSK", "streamingSK", "naiveSK"])
