@@ -17,6 +17,25 @@ namespace cvr {
 
 #define CVR_DEV __device__ __forceinline__
 
+// A pointer to global memory as the global address space.  The wave-pool
+// kernel keeps its launch parameters in LDS, so their pointers reach the code
+// as generic (flat) pointers, and flat loads, stores and atomics count in
+// lgkmcnt as well as vmcnt: every later LDS wait then also waits for them (a
+// batch's slot stores and framebuffer atomics stalled its LDS list updates).
+// Global instructions count in vmcnt only.
+template <class T>
+using gptr_t = __attribute__((address_space(1))) T*;
+template <class T>
+CVR_DEV gptr_t<T> gmem(T* p) {
+  return (gptr_t<T>)p;
+}
+typedef float cvr_f4v __attribute__((ext_vector_type(4)));
+CVR_DEV void gstore4(float4* p, float4 v) { *(gptr_t<cvr_f4v>)p = cvr_f4v{v.x, v.y, v.z, v.w}; }
+CVR_DEV float4 gload4(const float4* p) {
+  const cvr_f4v v = *(__attribute__((address_space(1))) const cvr_f4v*)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // ------------------------------------------------------------- vectors ----
 struct V3 {
   float x, y, z;
@@ -239,7 +258,7 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   const uint32_t per_block = 64u * L.samples;
   const uint32_t bq = fastdiv(u, L.div_block);
   uint32_t bl = queue_blocks_begin(L, q) + bq;
-  if (L.block_perm) bl = L.block_perm[bl];
+  if (L.block_perm) bl = gmem(L.block_perm)[bl];
   const uint32_t b = L.blk_off + __umul24(bl, L.blk_stride);
   const uint32_t rem = u - bq * per_block;
   const uint32_t s = rem >> 6, lane = rem & 63u;
@@ -775,12 +794,21 @@ CVR_DEV bool roulette(PathState& ps) {
 #ifndef CVR_DIAG_NO_SPLAT  // diagnostic builds only (tools/job_writes.sh): no framebuffer writes
 #define CVR_DIAG_NO_SPLAT 0
 #endif
+#ifndef CVR_DIAG_SPLAT_WG  // diagnostic builds only: workgroup-scope splat atomics (timing experiment)
+#define CVR_DIAG_SPLAT_WG 0
+#endif
 CVR_DEV void splat(const LaunchParams& L, const PathState& ps) {
   if (CVR_DIAG_NO_SPLAT) return;
-  float* px = reinterpret_cast<float*>(L.out + ps.image_id);
-  atomicAdd(px + 0, ps.T.x);
-  atomicAdd(px + 1, ps.T.y);
-  atomicAdd(px + 2, ps.T.z);
+  gptr_t<float> px = gmem(reinterpret_cast<float*>(L.out + ps.image_id));
+  if (CVR_DIAG_SPLAT_WG) {
+    __hip_atomic_fetch_add(px + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(px + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(px + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    __hip_atomic_fetch_add(px + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(px + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(px + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   px[3] = 1.0f;
 }
 

@@ -146,13 +146,13 @@ __device__ __forceinline__ void store_full(WavePool<kSlots, kSplit>& S, float4* 
   S.e[s] = make_uint2(ps.rng.v4, ps.rng.d);
   S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
   const float4 f = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
-  if constexpr (kSplit) gT[s] = f;
+  if constexpr (kSplit) gstore4(gT + s, f);
   else S.f[s] = f;
 }
 template <int kSlots, bool kSplit>
 __device__ __forceinline__ void load_full(const WavePool<kSlots, kSplit>& S, const float4* __restrict__ gT, uint32_t s,
                                           PathState& ps, Isect& is, uint32_t& nseg, float& t) {
-  const float4 f = kSplit ? gT[s] : S.f[s];
+  const float4 f = kSplit ? gload4(gT + s) : S.f[s];
   const float4 a = S.a[s], b = S.b[s];
   const uint4 c = S.c[s];
   const uint2 e = S.e[s];
@@ -524,6 +524,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
               for (uint32_t k = 0; k < L.n_queues; ++k) {
                 const uint32_t q = ((cqh >> 8) + k) % L.n_queues;
                 if ((dead >> q) & 1ull) continue;
+                // (a generic atomic: its global form costs the dense kernel ~40 VGPRs of
+                // pressure; lane 0 waits for its result right here anyway)
                 const uint32_t g = atomicAdd(L.queue + 16 * q, L.chunk);
                 if (g < queue_units(L, q)) {
                   b = g;
@@ -716,7 +718,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     // density evaluations: steps minus segments whose last step passed max_t
     const unsigned long long w[STAT_COUNT] = {S.cnt[STAT_PATHS], S.cnt[STAT_SEGMENTS], steps, steps - n_over,
                                               S.cnt[STAT_ALBEDO], S.cnt[STAT_ESCAPED], S.cnt[STAT_TRUNCATED], fetch};
-    if (lane < (uint32_t)STAT_COUNT && w[lane]) atomicAdd(L.stats + lane, w[lane]);
+    if (lane < (uint32_t)STAT_COUNT && w[lane])
+      __hip_atomic_fetch_add(gmem(L.stats + lane), w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #if CVR_TAILSTAMPS
   {
