@@ -136,7 +136,7 @@ struct cvr_ctx {
   uint32_t pool_tail = 16;
   int wpool_grid = 0, wpool_grid_sparse = 0;
   // wave-pool register/LDS budget in waves per SIMD (CVR_OPT_WAVES: 3, 4, 5);
-  // 0 = per medium: 5 dense (split slots), 4 sparse
+  // 0 = the default, 5 (dense and sparse, split slots)
   int wpool_waves = 0;
   int morton = 0;  // CVR_OPT_MORTON
   uint32_t swap_batch = 8;
@@ -222,7 +222,7 @@ bool morton_for(const cvr_ctx* c) { return c->morton > 0; }
 
 int wpool_waves_for(const cvr_ctx* c, bool sparse) {
   if (c->wpool_waves) return c->wpool_waves;
-  return sparse ? 4 : 5;
+  return 5;  // dense and sparse (split slots: DESIGN.md §6)
 }
 
 // Wave-pool grid of a launch of n_paths (one wave per workgroup): CVR_OPT_GRID,

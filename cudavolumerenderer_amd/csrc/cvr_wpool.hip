@@ -89,11 +89,12 @@ struct PoolSize {
   static_assert(4 * STAT_COUNT + 8 + 12 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
 #endif
 };
-// Sparse media (C5) keep the event part in LDS too: their cell-leaf pool
-// thrashes L2, so the split's T reads would go to HBM (C5: 156.8 ms split at
-// 4 waves, 153.7 at 5, vs 147 with T in LDS).
+// Sparse media (C5) split the slot too and run 5 waves per SIMD: 142.7 ms vs
+// 147.6 with the event part in LDS at 4 waves (round 3, once the global part's
+// loads and stores stopped being flat instructions that LDS waits also waited
+// for; round 2 measured 156.8 split at 4 waves, 153.7 at 5).
 #ifndef CVR_WPOOL_SPLIT_SPARSE
-#define CVR_WPOOL_SPLIT_SPARSE 0
+#define CVR_WPOOL_SPLIT_SPARSE 1
 #endif
 
 // One path per slot.  LDS holds what the track loop and the event code both
@@ -755,7 +756,9 @@ static const void* wpool_fn(int waves, bool sparse) {
 // carry none of the record code): the default register budgets.
 template <bool E>
 static const void* wpool_record_fn(int waves, bool sparse) {
-  if (sparse) return waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, true, true>) : nullptr;
+  if (sparse) return waves == 5   ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, true>)
+                    : waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, true, true>)
+                                 : nullptr;
   return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, false, true>) : nullptr;
 }
 

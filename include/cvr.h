@@ -73,7 +73,7 @@ typedef enum {
   CVR_OPT_CELLS = 9           /* 1 (default): corner-replicated density cells (8x density bytes
                                  in HBM, 2 x 16 B loads per Woodcock step); applies at set_medium */,
   CVR_OPT_WAVES = 10,         /* register/LDS budget in waves per SIMD: persistent kernel 4 (default), 5, 6,
-                                 8; wave-pool kernel 3, 4, 5, 6 (default: 5 dense, 4 sparse; 6 is dense only
+                                 8; wave-pool kernel 3, 4, 5, 6 (default: 5; 6 is dense only
                                  and spills) */
   CVR_OPT_ORDER = 11,         /* 2 (default): 8x8-pixel blocks, samples innermost, each XCD band's blocks in
                                  2-D Morton order; 1: the same blocks row-major; 0: path-id order */

@@ -55,7 +55,7 @@ def main():
         c.clear_output()
         c.launch_render()
         st = c.stats()
-    nw = cu * 4 * (4 if scene.is_sparse else 5)  # the wave-pool grid (one wave per workgroup)
+    nw = cu * 4 * 5  # the wave-pool grid (one wave per workgroup, 5 per SIMD)
     buf = (C.c_uint64 * (nw * 10))()
     lib.cvr_debug_tailstamps(c._h, buf, nw)
     s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 10).astype(np.int64)
