@@ -110,7 +110,7 @@ struct cvr_ctx {
   float4* d_pool_T = nullptr;       // wave-pool scheduler: event-only slot part (LaunchParams::pool_T)
   size_t pool_T_n = 0;
   uint32_t n_queues = 8;            // work-order bands (one per XCD)
-  uint32_t subqueues = 0;           // wave pool: queues per band (CVR_OPT_SUBQUEUES; 0 = by launch size)
+  uint32_t subqueues = 8;           // wave pool: queues per band (CVR_OPT_SUBQUEUES)
   int drain = -1;                   // wave pool: drain-mode event trigger (CVR_OPT_DRAIN; -1 = 1)
   int order = 2;                    // 1: pixel-block/sample-inner order when the launch allows it; 2: blocks
                                     // in 2-D Morton order within each band
@@ -339,16 +339,9 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
     uint32_t bands = c->n_queues < L.n_blocks ? c->n_queues : L.n_blocks;
     if (bands == 0) bands = 1;
     // sub-queues per band: the wave pool only, each with at least one block
-    // Sub-queues per band: small launches (block shards, dequeue chunks of 64..128 paths) spread
-    // their queue heads over 8 per band; a whole-image launch (>= 2048 paths per wave, chunks of
-    // 256) keeps one, so each XCD's waves work on one front of its band (C3 5.55 vs 5.77 ms,
-    // C2 flat; profiles/round3/ab/retune_sub_*.log)
-    uint32_t sub = c->subqueues;
-    if (sub == 0) {
-      const uint64_t grid = wpool_launch_grid(c, L.path_count);
-      sub = (grid && L.path_count / grid >= 2048) ? 1u : 8u;
-    }
-    if (scheduler_for(c) != 3) sub = 1u;
+    // Sub-queues per band (8 by default: C2 5.03 vs 5.07 ms with one, manix 2048^2 28.9 vs
+    // 29.2; C3 prefers one, 5.56 vs 5.60; profiles/round3/ab/sub3_*.log, c4sub.log)
+    uint32_t sub = scheduler_for(c) == 3 ? c->subqueues : 1u;
     while (sub > 1 && bands * sub > L.n_blocks) --sub;
     L.sub = sub;
     L.n_queues = bands * sub;
@@ -1124,7 +1117,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->n_queues = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_SUBQUEUES:
-      if (v < 0 || v > 8) return set_err(&c->err, CVR_ERR_INVALID, "subqueues must be 0..8");
+      if (v < 1 || v > 8) return set_err(&c->err, CVR_ERR_INVALID, "subqueues must be 1..8");
       c->subqueues = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_INFLIGHT:

@@ -98,9 +98,8 @@ typedef enum {
                                  (operator precedence, Utilities.cuh:129-132); 1 the intended
                                  (p - min)/extent, computed as fma(p, 1/extent, -min/extent).  The two
                                  agree for the unit box of VDB/Raw/MHD scenes. */
-  CVR_OPT_SUBQUEUES = 20,      /* wave-pool scheduler: work queues per XCD band (1..8; 0, the default:
-                                 8 for launches of fewer than 2048 paths per wave, else 1), each over a
-                                 contiguous part of the band, so that small dequeue chunks do not
+  CVR_OPT_SUBQUEUES = 20,      /* wave-pool scheduler: work queues per XCD band (1..8, default 8), each
+                                 over a contiguous part of the band, so that small dequeue chunks do not
                                  contend on one head.  Scheduling only. */
   CVR_OPT_INFLIGHT = 23,       /* wave-pool scheduler: renders the caller keeps in flight on this device
                                  (default 1).  Sets the grid of small launches (CVR_OPT_GRID 0): below 64
