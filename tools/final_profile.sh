@@ -21,11 +21,6 @@ step() {  # name seconds cmd...
 B="python3 bench.py --no-cpu-baseline"
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 600 python3 -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider
-step c2_bench 200 python3 bench.py --steps 20 --warmup 5
-step c1_bench 200 python3 bench.py --scene bucky --steps 20 --warmup 5
-step c3_bench 200 python3 bench.py --scene hetvol --steps 20 --warmup 5
-step c5_bench 400 python3 bench.py --scene cloud --steps 5 --warmup 1
-step c4_bench 400 $B --shard tiles --resolution 2048 2048 --iterations 256 --steps 2 --warmup 1
 for sc in manix hetvol cloud; do
   if [ $sc = cloud ]; then S="--steps 3 --warmup 1"; else S="--steps 10 --warmup 2"; fi
   step prof_$sc 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- $B --scene $sc $S
@@ -34,6 +29,16 @@ for sc in manix hetvol cloud; do
   step pmcw_$sc 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
   cp "$OUT/libcvr.sha256" "$OUT/pmcf_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcw_$sc/"
 done
+# fold the traffic passes into profiles/traffic.json here too, so the bench lines
+# below (same libcvr.so) carry their measured traffic
+python3 tools/traffic.py "$OUT/pmcf_manix" "$OUT/pmcw_manix" k_wpool_1024x1024_20it > /dev/null &&
+  python3 tools/traffic.py "$OUT/pmcf_hetvol" "$OUT/pmcw_hetvol" hetvol_k_wpool_1024x1024_20it > /dev/null &&
+  python3 tools/traffic.py "$OUT/pmcf_cloud" "$OUT/pmcw_cloud" cloud_k_wpool_4096x4096_20it > /dev/null || exit 1
+step c2_bench 200 python3 bench.py --steps 20 --warmup 5
+step c1_bench 200 python3 bench.py --scene bucky --steps 20 --warmup 5
+step c3_bench 200 python3 bench.py --scene hetvol --steps 20 --warmup 5
+step c5_bench 400 python3 bench.py --scene cloud --steps 5 --warmup 1
+step c4_bench 400 $B --shard tiles --resolution 2048 2048 --iterations 256 --steps 2 --warmup 1
 step pmc_a 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc_a" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
 step pmc_b 200 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc_b" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
 step pmc_c 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc_c" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
