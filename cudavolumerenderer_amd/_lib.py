@@ -29,7 +29,7 @@ SCENE_TYPES = {"Auto": 0, "MitsubaXml": 1, "Vdb": 2, "Raw": 3, "Mhd": 4, "VdbSpa
 OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1, 2, 3, 4, 5
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
-OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT = 18, 19, 20, 22, 23
+OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT, OPT_FRAME_FLUSH = 18, 19, 20, 22, 23, 24
 
 
 class CvrError(RuntimeError):
@@ -123,6 +123,7 @@ def load() -> C.CDLL:
         "cvr_trace_launch": (I32, [P, P, U64]),
         "cvr_image_to_host": (I32, [P, P, C.c_size_t, C.c_float, P]),
         "cvr_render_frame": (I32, [P, P, U32, C.POINTER(Stats)]),
+        "cvr_frame_flush_info": (I32, [P, C.POINTER(U32), C.POINTER(U32)]),
         "cvr_blocks_to_host": (I32, [P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float, P]),
         "cvr_launch_blocks": (I32, [P, P, P, P]),
         "cvr_set_seed": (I32, [P, U32]),
@@ -511,6 +512,13 @@ class Context:
             host_ptr = img.ctypes.data
         self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), parts, C.byref(st) if stats else None))
         return img, st
+
+    def frame_flush_info(self):
+        """(blocks the last render_frame's flusher waves stored in the launch, 0 if it
+        copied after the launch; calls that fell back to the copy) (cvr_frame_flush_info)."""
+        b, f = C.c_uint32(0), C.c_uint32(0)
+        self._c(load().cvr_frame_flush_info(self._h, C.byref(b), C.byref(f)))
+        return b.value, f.value
 
     def render_tiles(self, width, height, n_tiles=(1, 1), iterations=20, first_tile: int = 0,
                      tile_stride: int = 1, device_image: Optional[int] = None, host: bool = True):

@@ -169,6 +169,16 @@ struct cvr_ctx {
   hipEvent_t frame_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [0] cleared, [1 + k] band k rendered
   float4* d_frame = nullptr;
   size_t frame_px = 0;
+  // cvr_render_frame's in-launch output (CVR_OPT_FRAME_FLUSH, wave pool): [FrameFlush
+  // header | per-block ended-path counts], the flushers' status words (pinned), the
+  // header as last written, and the counts the next launch takes (null: none)
+  int frame_flush = 1;
+  unsigned char* d_flush = nullptr;
+  size_t flush_blocks = 0;
+  unsigned int* h_flush_status = nullptr;
+  cvr::FrameFlush flush_hdr{};
+  unsigned int* frame_done_active = nullptr;
+  uint32_t flush_last_blocks = 0, flush_fallbacks = 0;
 };
 
 #ifndef CVR_TAILSTAMPS
@@ -657,6 +667,8 @@ int cvr_destroy(cvr_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->frame_copy) (void)hipStreamDestroy(c->frame_copy);
   if (c->d_frame) (void)hipFree(c->d_frame);
+  if (c->d_flush) (void)hipFree(c->d_flush);
+  if (c->h_flush_status) (void)hipHostFree(c->h_flush_status);
   delete c;
   return CVR_OK;
 }
@@ -1124,6 +1136,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       if (v < 1 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "inflight must be 1..64");
       c->inflight = (uint32_t)v;
       return CVR_OK;
+    case CVR_OPT_FRAME_FLUSH:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "frame flush must be 0 or 1");
+      c->frame_flush = (int)v;
+      return CVR_OK;
     case CVR_OPT_DRAIN:
       if (v < -1 || v > 64) return set_err(&c->err, CVR_ERR_INVALID, "drain must be -1..64");
       c->drain = (int)v;
@@ -1313,6 +1329,13 @@ int cvr_launch_render(cvr_ctx* c) {
     }
     L.pool_T = c->d_pool_T;
     L.rec = c->d_rec_active;
+    if (c->frame_done_active) {
+      // in-launch output: the first kFrameFlushers workgroups flush, the rest render
+      if (L.rec || L.order != 1 || grid <= 4 * cvr::kFrameFlushers)
+        return set_err(&c->err, CVR_ERR_STATE, "in-launch output needs a pixel-block launch of > %u waves",
+                       4 * cvr::kFrameFlushers);
+      L.frame_done = c->frame_done_active;
+    }
     HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
@@ -1650,6 +1673,75 @@ static void copy_settings(cvr_ctx* d, const cvr_ctx* s) {
   d->pool_max = s->pool_max;
 }
 
+// cvr_render_frame with the in-launch output: the clear, the header and the block
+// counts, one launch whose flusher waves store the normalised blocks into the host
+// image (device address dhost), and the copy after the launch only if a flusher gave up.
+static int render_frame_flush(cvr_ctx* c, float* host_image, void* dhost, cvr_stats* stats) {
+  const uint32_t W = c->tile_w, H = c->tile_h;
+  const size_t px = (size_t)W * H, nb = (size_t)(W / 8u) * (H / 8u);
+  if (c->flush_blocks < nb) {
+    if (c->d_flush) (void)hipFree(c->d_flush);
+    c->d_flush = nullptr;
+    c->flush_blocks = 0;
+    HIP_TRY(c, hipMalloc(&c->d_flush, sizeof(cvr::FrameFlush) + nb * cvr::kDoneStride * sizeof(unsigned int)));
+    c->flush_blocks = nb;
+  }
+  if (!c->h_flush_status) {
+    HIP_TRY(c, hipHostMalloc(&c->h_flush_status, 64, hipHostMallocDefault));
+  }
+  if (!c->frame_ev[0])
+    for (auto& e : c->frame_ev) HIP_TRY(c, hipEventCreate(&e));
+  unsigned int* dstatus = nullptr;
+  HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&dstatus), c->h_flush_status, 0));
+  memset(c->h_flush_status, 0, 64);  // the previous frame has ended (its call synchronised)
+  c->flush_hdr = cvr::FrameFlush{};
+  c->flush_hdr.host = static_cast<float4*>(dhost);
+  c->flush_hdr.status = dstatus;
+  c->flush_hdr.host_w = W;
+  c->flush_hdr.scale = (float)c->iterations;
+  unsigned int* done = reinterpret_cast<unsigned int*>(c->d_flush + sizeof(cvr::FrameFlush));
+  HIP_TRY(c, hipMemsetAsync(c->d_out, 0, px * sizeof(float4), c->stream));  // initRenderState
+  HIP_TRY(c, hipMemcpyAsync(c->d_flush, &c->flush_hdr, sizeof(cvr::FrameFlush), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, hipMemsetAsync(done, 0, nb * cvr::kDoneStride * sizeof(unsigned int), c->stream));
+  HIP_TRY(c, hipEventRecord(c->frame_ev[0], c->stream));
+  c->frame_done_active = done;
+  int r = cvr_launch_render(c);
+  c->frame_done_active = nullptr;
+  if (r) return r;
+  HIP_TRY(c, hipEventRecord(c->frame_ev[1], c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  uint64_t stored = 0;
+  for (uint32_t f = 0; f < cvr::kFrameFlushers; ++f) stored += c->h_flush_status[f];
+  if (c->h_flush_status[cvr::kFrameFlushers] != 0 || stored != nb) {
+    // a flusher gave up: getImage the usual way (the framebuffer is complete)
+    ++c->flush_fallbacks;
+    c->flush_last_blocks = 0;
+    HIP_TRY(c, cvr::launch_image_to_host(reinterpret_cast<const float*>(c->d_out), static_cast<float*>(dhost),
+                                         px * 4, (float)c->iterations, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  } else {
+    c->flush_last_blocks = (uint32_t)stored;
+  }
+  (void)host_image;
+  c->seed = seed_after_resets(c, c->seed, 1);  // reset(): prepareForNextIterations
+  if (!stats) return CVR_OK;
+  cvr_stats acc{};
+  if ((r = cvr_get_stats(c, &acc))) return r;
+  float ms = 0.f;  // clear to the end of the launch
+  HIP_TRY(c, hipEventElapsedTime(&ms, c->frame_ev[0], c->frame_ev[1]));
+  acc.kernel_ms = ms;
+  c->last = acc;
+  *stats = acc;
+  return CVR_OK;
+}
+
+int cvr_frame_flush_info(const cvr_ctx* c, uint32_t* blocks, uint32_t* fallbacks) {
+  if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
+  if (blocks) *blocks = c->flush_last_blocks;
+  if (fallbacks) *fallbacks = c->flush_fallbacks;
+  return CVR_OK;
+}
+
 int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* stats) {
   if (!c || !host_image) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   int r = check_ready(c);
@@ -1680,6 +1772,18 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* s
       row0[k + 1] = k + 1 == parts ? brows : (uint32_t)((uint64_t)brows * acc / shares);
     }
   }
+  // in-launch output (CVR_OPT_FRAME_FLUSH): one part on the wave pool, and a host image
+  // the GPU can store into
+  void* dhost = nullptr;
+  if (c->frame_flush && parts == 1 && brows && scheduler_for(c) == 3 && !c->d_rec_active &&
+      wpool_waves_for(c, c->m.leaves != nullptr) == 5 && wpool_launch_grid(c, L0.path_count) > 4 * cvr::kFrameFlushers) {
+    if (hipHostGetDevicePointer(&dhost, host_image, 0) != hipSuccess) {
+      (void)hipGetLastError();  // pageable memory: not an error, the copy path below
+      dhost = nullptr;
+    }
+  }
+  if (dhost) return render_frame_flush(c, host_image, dhost, stats);
+  c->flush_last_blocks = 0;
   while (c->frame_kids.size() + 1 < parts) {
     cvr_ctx* k = nullptr;
     if ((r = cvr_create(c->device, c->kernel, &k))) return set_err(&c->err, r, "frame helper: %s", g_last_error.c_str());

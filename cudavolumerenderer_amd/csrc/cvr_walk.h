@@ -242,7 +242,33 @@ struct LaunchParams {
   const uint32_t* block_perm;
   // by tile_px, tile_w, 64*samples, blocks_x, n_queues
   FastDiv div_tile_px, div_tile_w, div_block, div_blocks_x, div_queues;
+  // cvr_render_frame's in-launch output (wave pool, order 1, whole samples; null
+  // otherwise): per tile block the number of its paths that have ended (block b at
+  // frame_done[kDoneStride * b]), preceded by the FrameFlush header (frame_header()).
+  // See cvr_wpool.hip, frame_flusher.
+  unsigned int* frame_done;
 };
+
+// Header of the in-launch output (64 bytes just below LaunchParams::frame_done).
+struct FrameFlush {
+  float4* host;          // device address of the pinned host image (the tile's pixels)
+  unsigned int* status;  // device address of pinned host words: [f] blocks flusher f stored,
+                         // [kFrameFlushers] flushers that gave up waiting
+  uint32_t host_w;       // host image row length in pixels
+  float scale;           // the Scale functor's divisor (iterations)
+  uint32_t pad[10];
+};
+static_assert(sizeof(FrameFlush) == 64, "FrameFlush is the 64-byte header below frame_done");
+constexpr uint32_t kFrameFlushers = 8;  // the first workgroups of a flushing launch
+// one count per 64-byte line: blocks dequeued together are counted by different
+// waves at the same time, and atomics on one line serialise at the memory side
+#ifndef CVR_DONE_STRIDE
+#define CVR_DONE_STRIDE 16
+#endif
+constexpr uint32_t kDoneStride = CVR_DONE_STRIDE;
+CVR_DEV const FrameFlush* frame_header(const unsigned int* done) {
+  return reinterpret_cast<const FrameFlush*>(done) - 1;
+}
 
 // Map the u-th work unit of queue q to a path id (order 1), see LaunchParams.
 // n_blocks * q < 2^24 (n_blocks <= 2^18, q <= 64).
@@ -265,6 +291,16 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   const uint32_t by = fastdiv(b, L.div_blocks_x);
   const uint32_t px = (b - by * L.blocks_x) * 8u + (lane & 7u), py = by * 8u + (lane >> 3);
   return L.path_first + s * L.tile_px + py * L.tile_w + px;
+}
+// Tile block of the launch's bl-th block (order 1), as unit_to_path maps it.
+CVR_DEV uint32_t launch_block_tile(const LaunchParams& L, uint32_t bl) {
+  if (L.block_perm) bl = gmem(L.block_perm)[bl];
+  return L.blk_off + __umul24(bl, L.blk_stride);
+}
+// Tile block (8x8 pixels, row-major) of a pixel of the tile.
+CVR_DEV uint32_t tile_block_of(const LaunchParams& L, uint32_t image_id) {
+  const uint32_t py = fastdiv(image_id, L.div_tile_w), px = image_id - py * L.tile_w;
+  return (py >> 3) * L.blocks_x + (px >> 3);
 }
 
 enum {

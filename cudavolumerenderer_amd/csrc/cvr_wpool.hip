@@ -86,7 +86,7 @@ struct PoolSize {
   static constexpr int value = CVR_WPOOL_SLOTS;
 #else
   static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT) / (kSplit ? 64 : 80);
-  static_assert(4 * STAT_COUNT + 8 + 12 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
+  static_assert(4 * STAT_COUNT + 8 + 12 + 4 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
 #endif
 };
 // Sparse media (C5) split the slot too and run 5 waves per SIMD: 142.7 ms vs
@@ -123,6 +123,10 @@ struct WavePool {
   // (LDS, not SGPRs: only the regeneration code reads it, and the kernel has no scalar
   // registers to spare)
   uint32_t cur[3];
+  // in-launch output (LaunchParams::frame_done): the last batch's ended paths, not yet
+  // counted: ln stack entries [pend & 0xFF, + pend >> 8), each slot's meta holding its
+  // pixel (image_id)
+  uint32_t pend;
 };
 constexpr uint32_t kCurExhausted = 1u << 16;
 
@@ -226,14 +230,169 @@ __device__ __forceinline__ const LaunchParams& fresh(const LaunchParams& L) {
   return *(const LaunchParams*)p;
 }
 
+// ---- in-launch output (cvr_render_frame) -----------------------------------
+// getImage (CudaVolPath.cpp:339-347, ImageBufferTransfer.cu:61-78: Scale, then
+// the D->H copy) without a copy after the launch: each wave counts its ended
+// paths per 8x8 tile block, and kFrameFlushers flusher waves store a block's
+// normalised pixels into the pinned host image as soon as all 64 * samples of
+// its paths have ended, while the launch goes on.
+//
+// Ordering: the framebuffer atomics (splat) and the block counts are agent-
+// scope atomics, performed at the memory side.  A batch's ended paths are
+// counted at the next batch (or at the wave's exit): it first waits for all of
+// the wave's outstanding memory operations, so a full count means every splat
+// of the block has been performed, and the flusher reads the pixels with
+// atomics too.  Most of a batch's ended paths lie in lane 0's block (the wave's
+// current chunk): their count is one atomic, issued at the end of the counting
+// batch beside that batch's splats, so that no memory wait of the batch's own
+// loads waits for it; the other lanes add 1 each at once.
+constexpr unsigned kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+constexpr uint32_t kPendAgg = 0x80000000u;  // S.pend holds kPendAgg | block << 7 | count
+
+template <int kSlots, bool kSplit>
+__device__ __forceinline__ uint32_t count_ended(const WavePool<kSlots, kSplit>& S, const LaunchParams& L, uint32_t pend,
+                                                uint32_t lane) {
+  const uint32_t base = pend & 0xFFu, n = pend >> 8;
+#ifndef CVR_DIAG_COUNT  // diagnostic builds: bit 0 no wait, bit 1 no atomics, bit 2 no counting
+#define CVR_DIAG_COUNT 0
+#endif
+  if (!(CVR_DIAG_COUNT & 1)) __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  uint32_t blk = 0;
+  if (lane < n) blk = tile_block_of(fresh(L), S.meta[S.ln[base + lane]]);
+  const uint32_t b0 = __builtin_amdgcn_readfirstlane(blk);
+  const unsigned long long same = __ballot(lane < n && blk == b0);
+  if (!(CVR_DIAG_COUNT & 2) && lane < n && blk != b0)
+    __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * blk), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return kPendAgg | b0 << 7 | (uint32_t)__popcll(same);
+}
+__device__ __forceinline__ void add_counted(const LaunchParams& L, uint32_t agg) {
+  if (CVR_DIAG_COUNT & 2) return;
+  __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * ((agg & ~kPendAgg) >> 7)), agg & 0x7Fu,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Up to 8 tile blocks' pixels (one per lane in each block), normalised, into the
+// host image: all reads first (24 atomics in flight per lane), then the stores.
+__device__ __forceinline__ void store_blocks(const LaunchParams& L, const FrameFlush& F, const uint32_t (&b)[8], uint32_t nb,
+                                             uint32_t lane) {
+  float v[8][3];
+  size_t pix[8];
+#pragma unroll
+  for (uint32_t k = 0; k < 8u; ++k) {
+    if (k < nb) {
+      const uint32_t by = fastdiv(b[k], L.div_blocks_x), bx = b[k] - by * L.blocks_x;
+      const uint32_t px = bx * 8u + (lane & 7u), py = by * 8u + (lane >> 3);
+      pix[k] = (size_t)py * L.tile_w + px;
+      gptr_t<float> src = gmem(reinterpret_cast<float*>(L.out + pix[k]));
+#pragma unroll
+      for (int c = 0; c < 3; ++c) v[k][c] = __hip_atomic_fetch_add(src + c, 0.0f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < 8u; ++k) {
+    if (k < nb) {
+      const float x = v[k][0], y = v[k][1], z = v[k][2];
+      // w: splat's plain store of 1 (Utilities.cuh:21) may still sit in another XCD's L2.
+      // It is 1 exactly when some path escaped to the pixel, and then the rgb sum is not
+      // zero (or NaN): an escaping path's throughput has a positive component, since
+      // roulette ends every path whose components are all zero (p = 0 < xi).
+      const float w = (x != 0.0f || y != 0.0f || z != 0.0f) ? 1.0f : 0.0f;
+      // the tile is the host image (cvr_render_frame: host_w = tile_w)
+      float4* dst = F.host + pix[k];
+      __builtin_nontemporal_store(x / F.scale, &dst->x);
+      __builtin_nontemporal_store(y / F.scale, &dst->y);
+      __builtin_nontemporal_store(z / F.scale, &dst->z);
+      __builtin_nontemporal_store(w / F.scale, &dst->w);
+    }
+  }
+}
+
+// Flusher wave f follows queues f, f + 8, ..., f + 56 through their blocks in
+// dequeue order: lane l looks at block cur + (l >> 3) of queue f + 8 (l & 7), so a
+// pass polls a window of 8 blocks per queue and stores every block in it whose
+// count is full (a block that ends late does not hold up the ones behind it);
+// stored blocks are marked in their count (kFlushed) and each queue's cursor
+// moves past its leading stored blocks.  A flusher that sees no block finish for
+// a second gives up (status word kFrameFlushers): the host then normalises and
+// copies the image after the launch.
+constexpr unsigned long long kFlushPatience = 100000000ull;  // s_memrealtime ticks (100 MHz)
+constexpr unsigned int kFlushed = 0x80000000u;
+#ifndef CVR_DIAG_FLUSH  // diagnostic builds: 1 = flushers store nothing (the host copies after the launch)
+#define CVR_DIAG_FLUSH 0
+#endif
+__device__ void frame_flusher(const LaunchParams& L) {
+  if (CVR_DIAG_FLUSH == 1) return;
+  const FrameFlush F = *frame_header(L.frame_done);
+  const uint32_t lane = threadIdx.x, f = blockIdx.x;
+  const uint32_t quota = 64u * L.samples, qi = lane & 7u, off = lane >> 3, q = f + kFrameFlushers * qi;
+  uint32_t cur = 0, end = 0, stored = 0;  // this lane's queue (all 8 lanes of a queue agree)
+  if (q < L.n_queues) {
+    cur = queue_blocks_begin(L, q);
+    end = queue_blocks_begin(L, q + 1u);
+  }
+  unsigned long long last = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    if (__ballot(cur < end) == 0ull) break;
+    const bool mine = cur + off < end;
+    uint32_t tb = 0, v = 0;
+    if (mine) {
+      tb = launch_block_tile(L, cur + off);
+      v = __hip_atomic_fetch_add(gmem(L.frame_done + kDoneStride * tb), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool ready = mine && v < kFlushed && v >= quota;
+    unsigned long long rm = __ballot(ready);
+    const unsigned long long settled = __ballot(mine && v >= quota);  // stored before or now
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    const bool any_ready = rm != 0ull;
+    while (rm != 0ull) {  // eight blocks per store_blocks call
+      uint32_t bsel[8], nb = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < 8u; ++k) {
+        if (rm != 0ull) {
+          bsel[k] = __builtin_amdgcn_readlane(tb, (uint32_t)__builtin_ctzll(rm));
+          rm &= rm - 1ull;
+          ++nb;
+        }
+      }
+      store_blocks(L, F, bsel, nb, lane);
+      stored += nb;
+    }
+    if (ready) __hip_atomic_fetch_or(gmem(L.frame_done + kDoneStride * tb), kFlushed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // each queue's cursor moves past its leading settled blocks (window bits qi, qi + 8, ...)
+    uint32_t lead = 0;
+#pragma unroll
+    for (uint32_t o = 0; o < 8u; ++o)
+      if (lead == o && ((settled >> (qi + 8u * o)) & 1ull)) ++lead;
+    cur += lead;
+    if (any_ready) {
+      last = now;
+    } else if (__ballot(lead != 0u) == 0ull) {
+      if (now - last > kFlushPatience) {
+        if (lane == 0) __hip_atomic_store(F.status + kFrameFlushers, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(32);
+    }
+  }
+  if (lane == 0) __hip_atomic_store(F.status + f, stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace
 
-template <bool kScatterEps, int kWaves, bool kSparse, bool kRecord>
+// kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
+// the other instances carry none of its code.
+template <bool kScatterEps, int kWaves, bool kSparse, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr bool kSplit = !kSparse || CVR_WPOOL_SPLIT_SPARSE;
   constexpr int kSlots = PoolSize<kWaves, kSplit>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
   // branches of the walk code fold away and take no scalar registers.
+  if constexpr (kFlush) {
+    if (Lk.frame_done != nullptr && blockIdx.x < kFrameFlushers) {
+      frame_flusher(Lk);
+      return;
+    }
+  }
   MediumParams m = mk;
   if constexpr (!kSparse) {
     m.leaves = nullptr;
@@ -258,7 +417,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   // across the track loop); the track loop counts steps and fetches per lane.
   uint32_t c_steps = 0, c_fetch = 0;
   if (lane < (uint32_t)STAT_COUNT) S.cnt[lane] = 0u;
-  if (lane == 0) S.dead = 0ull;
+  if (lane == 0) {
+    S.dead = 0ull;
+    S.pend = 0u;
+  }
   uint32_t n_over = 0;  // wave-uniform: segments whose last Woodcock step passed max_t
   // home queue: the XCD's band, and within it sub-queue (workgroup / 8) mod sub
   // (workgroups are dealt round-robin over the 8 XCDs)
@@ -402,6 +564,13 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
     // ================================================= EVENT ==============
     __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
+    if constexpr (kFlush) {
+      const uint32_t pend = S.pend;  // the last batch's ended paths (in-launch output)
+      if (!(CVR_DIAG_COUNT & 4) && pend != 0u) {
+        const uint32_t agg = count_ended(S, L, pend, lane);
+        if (lane == 0) S.pend = agg;
+      }
+    }
 #if CVR_TAILSTAMPS
     ++ts_n_ev;
     if (S.cur[2] & kCurExhausted) ts_bstart = __builtin_amdgcn_s_memrealtime();
@@ -576,6 +745,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           if (L.max_segments && nseg >= L.max_segments) {
             truncated = true;
             to_ln = true;
+            if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
             if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);
           } else {
             ++nseg;
@@ -584,6 +754,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
               splat(L, ps);
               escaped = true;
               to_ln = true;
+              if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
               if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
             } else if (is.inside) {
               store_full(S, L.pool_T + (size_t)blockIdx.x * kSlots, s, ps, is, nseg);
@@ -622,6 +793,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
       if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {  // the path died in roulette
         to_ln = true;
+        if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
         if (kRecord) record_end<kSlots>(L, s, ps, 0u, nseg);
       }
       // ---- next segment: AABB test of the survivors ----------------------
@@ -629,6 +801,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         if (L.max_segments && nseg >= L.max_segments) {
           truncated = true;
           to_ln = true;
+          if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
           if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);
         } else {
           ++nseg;
@@ -637,6 +810,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             splat(L, ps);
             escaped = true;
             to_ln = true;
+            if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
             if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
           } else {
             store_full(S, gT, s, ps, is, nseg);
@@ -664,6 +838,16 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       if (to_ready) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)s;
       if (to_lb) S.lb[n_lb + lane_rank(mb)] = (uint8_t)s;
       if (to_ln) S.ln[n_ln + lane_rank(mn)] = (uint8_t)s;
+      if constexpr (kFlush) {
+        // in-launch output: the ended paths (their slots' meta holds the pixel) are counted
+        // at the next batch
+        if (lane == 0) {
+          const uint32_t agg = S.pend;  // lane 0's block count of the last batch, beside this batch's splats
+          if (agg != 0u) add_counted(L, agg);
+          if (agg != 0u || mn != 0ull)
+            S.pend = mn != 0ull ? n_ln | (uint32_t)__popcll(mn) << 8 : 0u;
+        }
+      }
       n_ready += (uint32_t)__popcll(mr);
       n_lb += (uint32_t)__popcll(mb);
       n_ln += (uint32_t)__popcll(mn);
@@ -708,6 +892,13 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
   }
 
+  if constexpr (kFlush) {
+    const uint32_t pend = S.pend;  // raw: the last batch's ended paths
+    if (pend != 0u) {
+      const uint32_t agg = count_ended(S, L, pend, lane);
+      if (lane == 0) add_counted(L, agg);
+    }
+  }
   // ---- counters ------------------------------------------------------------
   {
     unsigned long long steps = c_steps, fetch = c_fetch;
@@ -744,31 +935,36 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 }
 
 template <bool E>
-static const void* wpool_fn(int waves, bool sparse) {
-  if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, false>)
-                                 : reinterpret_cast<const void*>(&k_wpool<E, 4, true, false>);
-  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false, false>);
-  if (waves == 6) return reinterpret_cast<const void*>(&k_wpool<E, 6, false, false>);
-  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false, false>);
-  return reinterpret_cast<const void*>(&k_wpool<E, 4, false, false>);
+static const void* wpool_fn(int waves, bool sparse, bool flush = false) {
+  if (flush) return waves != 5 ? nullptr
+                    : sparse   ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, false, true>)
+                               : reinterpret_cast<const void*>(&k_wpool<E, 5, false, false, true>);
+  if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, false, false>)
+                                 : reinterpret_cast<const void*>(&k_wpool<E, 4, true, false, false>);
+  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false, false, false>);
+  if (waves == 6) return reinterpret_cast<const void*>(&k_wpool<E, 6, false, false, false>);
+  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false, false, false>);
+  return reinterpret_cast<const void*>(&k_wpool<E, 4, false, false, false>);
 }
 // Record instances (cvr_trace_launch; debug only, so the production kernels
 // carry none of the record code): the default register budgets.
 template <bool E>
 static const void* wpool_record_fn(int waves, bool sparse) {
-  if (sparse) return waves == 5   ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, true>)
-                    : waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, true, true>)
+  if (sparse) return waves == 5   ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, true, false>)
+                    : waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, true, true, false>)
                                  : nullptr;
-  return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, false, true>) : nullptr;
+  return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, false, true, false>) : nullptr;
 }
 
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
                         hipStream_t s) {
   if (L.path_count == 0) return hipSuccess;
   const bool sparse = m.leaves != nullptr;
+  const bool flush = L.frame_done != nullptr;
+  if (L.rec && flush) return hipErrorInvalidValue;
   const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
-                         : (scatter_eps ? wpool_fn<true>(waves, sparse) : wpool_fn<false>(waves, sparse));
-  if (!fn) return hipErrorInvalidValue;  // no record instance for this register budget
+                         : (scatter_eps ? wpool_fn<true>(waves, sparse, flush) : wpool_fn<false>(waves, sparse, flush));
+  if (!fn) return hipErrorInvalidValue;  // no record / in-launch output instance for this register budget
   MediumParams mm = m;
   LaunchParams ll = L;
   void* args[] = {&mm, &ll};

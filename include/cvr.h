@@ -106,6 +106,11 @@ typedef enum {
                                  paths per wave of the occupancy grid half of it (a quarter with renders
                                  in flight), below 1024 paths per wave half of it with renders in flight,
                                  else all of it.  Scheduling only. */
+  CVR_OPT_FRAME_FLUSH = 24,    /* cvr_render_frame, one part, wave-pool scheduler, pinned or registered
+                                 host image: 1 (default) the launch itself stores each 8x8 block's
+                                 normalised pixels into the host image once all its paths have
+                                 ended (cvr_frame_flush_info); 0 normalise + copy after the launch.
+                                 Same image either way (C2: 5.21 vs 5.34 ms per call). */
   /* 21: unused (a drain-time path migration between waves, measured slower: DESIGN.md §6) */
   CVR_OPT_DRAIN = 22,          /* wave-pool scheduler, once the queues are empty: an event batch runs as
                                  soon as the waiting segments x d >= the tracking ones (d = 0: only when
@@ -287,8 +292,18 @@ int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats,
  * block shards) render as one part.  Afterwards the seed has advanced as the
  * reference's reset() advances it (cvr_reset).  stats (may be NULL, which
  * saves a synchronous counter read per band): the summed counters;
- * kernel_ms = from the clear to the end of the last band. */
+ * kernel_ms = from the clear to the end of the last band.  With one part on
+ * the wave-pool scheduler (5 waves per SIMD) and a pinned or registered host
+ * image the copy happens inside the launch (CVR_OPT_FRAME_FLUSH, default on):
+ * eight flusher waves store
+ * each 8x8 block, normalised, as soon as all of its paths have ended, so the
+ * image is complete when the kernel ends; if a flusher gives up (no block
+ * finished for a second) the call copies the image the usual way instead. */
 int cvr_render_frame(cvr_ctx* ctx, float* host_image, uint32_t parts, cvr_stats* stats);
+/* The last cvr_render_frame's in-launch output: blocks the flushers stored (0
+ * if the call copied after the launch) and the number of calls so far that
+ * fell back to the copy because a flusher gave up. */
+int cvr_frame_flush_info(const cvr_ctx* ctx, uint32_t* blocks, uint32_t* fallbacks);
 /* Extension (multi-GPU output): the pixels of block shard (rank, world) of a
  * width x height float4 image (cvr_set_block_shard: 8x8 blocks rank,
  * rank + world, ..., row-major; sides multiples of 8), divided by `scale`,

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """cvr_render_frame in a process with one context (no other streams): ms per
-synchronous render for 1, 2 and 3 bands, repeated (C2 by default).
+synchronous render, repeated (C2 by default), for the variants named in
+--variants: flush (one launch, in-launch output), copy (one launch, normalise +
+copy after it), bands2 / bands3 (2 / 3 bands of block rows, copies overlapped).
 
-  python tools/frame_probe.py [--scene manix] [--reps 20]
+  python tools/frame_probe.py [--scene manix] [--reps 20] [--variants flush,copy]
 """
 import argparse
 import os
@@ -20,9 +22,14 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="flush,copy,bands2,bands3")
+    ap.add_argument("--lib", default=None, help="alternative libcvr.so (experiment builds)")
     a = ap.parse_args()
     import torch
     import cudavolumerenderer_amd as cvr
+    if a.lib:
+        from cudavolumerenderer_amd import _lib as lb
+        lb.LIB_PATH = os.path.abspath(a.lib)
     scene = cvr.Scene.synthetic(a.scene)
     W = H = a.res
     iv, r2v = cvr.default_camera(W, H)
@@ -33,17 +40,20 @@ def main():
     c.set_resolution(W, H)
     c.set_iterations(a.iters)
     host = torch.empty(W * H * 4, dtype=torch.float32, pin_memory=True)
+    table = {"flush": (1, 1), "copy": (1, 0), "bands2": (2, 0), "bands3": (3, 0)}
     for rnd in range(a.rounds):
-        for parts in (1, 2, 3):
+        for v in a.variants.split(","):
+            parts, flush = table[v]
+            c.set_option(cvr.OPT_FRAME_FLUSH, flush)
             for _ in range(3):
-                c.render_frame(host.data_ptr(), parts)
+                c.render_frame(host.data_ptr(), parts, stats=False)
             t0 = time.perf_counter()
-            ks = 0.0
             for _ in range(a.reps):
-                _, st = c.render_frame(host.data_ptr(), parts)
-                ks += st.kernel_ms
+                c.render_frame(host.data_ptr(), parts, stats=False)
             ms = (time.perf_counter() - t0) / a.reps * 1e3
-            print(f"round {rnd} parts {parts}: {ms:.3f} ms per render (clear..last band {ks / a.reps:.3f} ms), "
+            _, st = c.render_frame(host.data_ptr(), parts)
+            print(f"round {rnd} {v:6s}: {ms:.3f} ms per render (one more with counters: clear..end "
+                  f"{st.kernel_ms:.3f} ms, flushed blocks {c.frame_flush_info()}), "
                   f"{W * H * a.iters / ms / 1e3:.1f} Msamples/s", flush=True)
 
 
