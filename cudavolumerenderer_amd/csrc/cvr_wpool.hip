@@ -93,6 +93,9 @@ struct PoolSize {
 // 147.6 with the event part in LDS at 4 waves (round 3, once the global part's
 // loads and stores stopped being flat instructions that LDS waits also waited
 // for; round 2 measured 156.8 split at 4 waves, 153.7 at 5).
+#ifndef CVR_SPARSE_SPECIALISE
+#define CVR_SPARSE_SPECIALISE 1
+#endif
 #ifndef CVR_WPOOL_SPLIT_SPARSE
 #define CVR_WPOOL_SPLIT_SPARSE 1
 #endif
@@ -400,6 +403,15 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
     m.scoarse = nullptr;
+  } else if (CVR_SPARSE_SPECIALISE) {
+    // and sparse instances see the dense pointers as constant null (a sparse medium
+    // has leaves, brick words and no dense grids; two-level bounds are a build option)
+    m.density = nullptr;
+    m.albedo = nullptr;
+    m.bounds = nullptr;
+    __builtin_assume(m.leaves != nullptr);
+    __builtin_assume(m.sbounds != nullptr);
+    if (!CVR_SPARSE_2LEVEL) m.scoarse = nullptr;
   }
   static_assert(sizeof(WavePool<kSlots, kSplit>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves, kSplit>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
