@@ -382,10 +382,15 @@ __device__ void frame_flusher(const LaunchParams& L) {
 
 }  // namespace
 
+// kMed: the medium layout the instance is compiled for (kMedDense any dense medium,
+// kMedSparse leaves + brick words, kMedDenseFull a dense medium with density cells
+// and brick bounds, the defaults: its null checks fold away, C2 -0.6%, C3 -1.8%).
 // kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
 // the other instances carry none of its code.
-template <bool kScatterEps, int kWaves, bool kSparse, bool kRecord, bool kFlush>
+enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2 };
+template <bool kScatterEps, int kWaves, int kMed, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
+  constexpr bool kSparse = kMed == kMedSparse;
   constexpr bool kSplit = !kSparse || CVR_WPOOL_SPLIT_SPARSE;
   constexpr int kSlots = PoolSize<kWaves, kSplit>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
@@ -403,6 +408,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
     m.scoarse = nullptr;
+    if constexpr (kMed == kMedDenseFull) {
+      __builtin_assume(m.cells != nullptr);
+      __builtin_assume(m.bounds != nullptr);
+    }
   } else if (CVR_SPARSE_SPECIALISE) {
     // and sparse instances see the dense pointers as constant null (a sparse medium
     // has leaves, brick words and no dense grids; two-level bounds are a build option)
@@ -946,26 +955,31 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
 }
 
+// Instances: 5 waves per SIMD (the default budget) for every medium layout, with and
+// without the in-launch output; the other budgets for the generic layouts.
 template <bool E>
-static const void* wpool_fn(int waves, bool sparse, bool flush = false) {
-  if (flush) return waves != 5 ? nullptr
-                    : sparse   ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, false, true>)
-                               : reinterpret_cast<const void*>(&k_wpool<E, 5, false, false, true>);
-  if (sparse) return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, false, false>)
-                                 : reinterpret_cast<const void*>(&k_wpool<E, 4, true, false, false>);
-  if (waves == 5) return reinterpret_cast<const void*>(&k_wpool<E, 5, false, false, false>);
-  if (waves == 6) return reinterpret_cast<const void*>(&k_wpool<E, 6, false, false, false>);
-  if (waves == 3) return reinterpret_cast<const void*>(&k_wpool<E, 3, false, false, false>);
-  return reinterpret_cast<const void*>(&k_wpool<E, 4, false, false, false>);
+static const void* wpool_fn(int waves, bool sparse, bool full, bool flush = false) {
+#define CVR_WP(W, M, F) reinterpret_cast<const void*>(&k_wpool<E, W, M, false, F>)
+  if (waves == 5) {
+    if (sparse) return flush ? CVR_WP(5, kMedSparse, true) : CVR_WP(5, kMedSparse, false);
+    if (full) return flush ? CVR_WP(5, kMedDenseFull, true) : CVR_WP(5, kMedDenseFull, false);
+    return flush ? CVR_WP(5, kMedDense, true) : CVR_WP(5, kMedDense, false);
+  }
+  if (flush) return nullptr;
+  if (sparse) return CVR_WP(4, kMedSparse, false);
+  if (waves == 6) return CVR_WP(6, kMedDense, false);
+  if (waves == 3) return CVR_WP(3, kMedDense, false);
+  return CVR_WP(4, kMedDense, false);
+#undef CVR_WP
 }
 // Record instances (cvr_trace_launch; debug only, so the production kernels
-// carry none of the record code): the default register budgets.
+// carry none of the record code): the default register budgets, generic layouts.
 template <bool E>
 static const void* wpool_record_fn(int waves, bool sparse) {
-  if (sparse) return waves == 5   ? reinterpret_cast<const void*>(&k_wpool<E, 5, true, true, false>)
-                    : waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, true, true, false>)
+  if (sparse) return waves == 5   ? reinterpret_cast<const void*>(&k_wpool<E, 5, kMedSparse, true, false>)
+                    : waves == 4 ? reinterpret_cast<const void*>(&k_wpool<E, 4, kMedSparse, true, false>)
                                  : nullptr;
-  return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, false, true, false>) : nullptr;
+  return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, kMedDense, true, false>) : nullptr;
 }
 
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
@@ -973,9 +987,10 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   if (L.path_count == 0) return hipSuccess;
   const bool sparse = m.leaves != nullptr;
   const bool flush = L.frame_done != nullptr;
+  const bool full = !sparse && m.cells != nullptr && m.bounds != nullptr;
   if (L.rec && flush) return hipErrorInvalidValue;
   const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
-                         : (scatter_eps ? wpool_fn<true>(waves, sparse, flush) : wpool_fn<false>(waves, sparse, flush));
+                         : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush) : wpool_fn<false>(waves, sparse, full, flush));
   if (!fn) return hipErrorInvalidValue;  // no record / in-launch output instance for this register budget
   MediumParams mm = m;
   LaunchParams ll = L;
@@ -993,7 +1008,7 @@ uint32_t wpool_slots(int waves, bool sparse) {
 }
 
 hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu) {
-  const void* fn = scatter_eps ? wpool_fn<true>(waves, sparse) : wpool_fn<false>(waves, sparse);
+  const void* fn = scatter_eps ? wpool_fn<true>(waves, sparse, false) : wpool_fn<false>(waves, sparse, false);
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, 0);
 }
 
