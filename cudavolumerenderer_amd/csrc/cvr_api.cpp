@@ -177,6 +177,7 @@ struct cvr_ctx {
   size_t flush_blocks = 0;
   unsigned int* h_flush_status = nullptr;
   cvr::FrameFlush flush_hdr{};
+  bool flush_hdr_valid = false;  // d_flush holds flush_hdr
   unsigned int* frame_done_active = nullptr;
   uint32_t flush_last_blocks = 0, flush_fallbacks = 0;
 };
@@ -1685,6 +1686,7 @@ static int render_frame_flush(cvr_ctx* c, float* host_image, void* dhost, cvr_st
     c->flush_blocks = 0;
     HIP_TRY(c, hipMalloc(&c->d_flush, sizeof(cvr::FrameFlush) + nb * cvr::kDoneStride * sizeof(unsigned int)));
     c->flush_blocks = nb;
+    c->flush_hdr_valid = false;
   }
   if (!c->h_flush_status) {
     HIP_TRY(c, hipHostMalloc(&c->h_flush_status, 64, hipHostMallocDefault));
@@ -1694,14 +1696,21 @@ static int render_frame_flush(cvr_ctx* c, float* host_image, void* dhost, cvr_st
   unsigned int* dstatus = nullptr;
   HIP_TRY(c, hipHostGetDevicePointer(reinterpret_cast<void**>(&dstatus), c->h_flush_status, 0));
   memset(c->h_flush_status, 0, 64);  // the previous frame has ended (its call synchronised)
-  c->flush_hdr = cvr::FrameFlush{};
-  c->flush_hdr.host = static_cast<float4*>(dhost);
-  c->flush_hdr.status = dstatus;
-  c->flush_hdr.host_w = W;
-  c->flush_hdr.scale = (float)c->iterations;
+  cvr::FrameFlush hdr{};
+  hdr.host = static_cast<float4*>(dhost);
+  hdr.status = dstatus;
+  hdr.host_w = W;
+  hdr.scale = (float)c->iterations;
+  // the header only travels when it changed (the same host image frame after frame: none)
+  const bool send_hdr = !c->flush_hdr_valid || memcmp(&hdr, &c->flush_hdr, sizeof(hdr)) != 0;
+  c->flush_hdr = hdr;
   unsigned int* done = reinterpret_cast<unsigned int*>(c->d_flush + sizeof(cvr::FrameFlush));
   HIP_TRY(c, hipMemsetAsync(c->d_out, 0, px * sizeof(float4), c->stream));  // initRenderState
-  HIP_TRY(c, hipMemcpyAsync(c->d_flush, &c->flush_hdr, sizeof(cvr::FrameFlush), hipMemcpyHostToDevice, c->stream));
+  if (send_hdr) {
+    c->flush_hdr_valid = false;
+    HIP_TRY(c, hipMemcpyAsync(c->d_flush, &c->flush_hdr, sizeof(cvr::FrameFlush), hipMemcpyHostToDevice, c->stream));
+    c->flush_hdr_valid = true;
+  }
   HIP_TRY(c, hipMemsetAsync(done, 0, nb * cvr::kDoneStride * sizeof(unsigned int), c->stream));
   HIP_TRY(c, hipEventRecord(c->frame_ev[0], c->stream));
   c->frame_done_active = done;

@@ -264,8 +264,23 @@ __device__ __forceinline__ uint32_t count_ended(const WavePool<kSlots, kSplit>& 
   if (lane < n) blk = tile_block_of(fresh(L), S.meta[S.ln[base + lane]]);
   const uint32_t b0 = __builtin_amdgcn_readfirstlane(blk);
   const unsigned long long same = __ballot(lane < n && blk == b0);
-  if (!(CVR_DIAG_COUNT & 2) && lane < n && blk != b0)
+#ifndef CVR_COUNT_AGG2
+#define CVR_COUNT_AGG2 1
+#endif
+  const bool rest = lane < n && blk != b0;
+  if (CVR_COUNT_AGG2) {  // a second block (the wave's previous chunk) with one atomic too
+    const unsigned long long rm = __ballot(rest);
+    if (rm != 0ull) {
+      const uint32_t first = (uint32_t)__builtin_ctzll(rm);
+      const uint32_t b1 = __builtin_amdgcn_readlane(blk, first);
+      const unsigned long long s1 = __ballot(rest && blk == b1);
+      if (!(CVR_DIAG_COUNT & 2) && (lane == first || (rest && blk != b1)))
+        __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * blk), lane == first ? (unsigned int)__popcll(s1) : 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (!(CVR_DIAG_COUNT & 2) && rest) {
     __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * blk), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   return kPendAgg | b0 << 7 | (uint32_t)__popcll(same);
 }
 __device__ __forceinline__ void add_counted(const LaunchParams& L, uint32_t agg) {
