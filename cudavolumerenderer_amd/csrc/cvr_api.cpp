@@ -1138,7 +1138,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->inflight = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_FRAME_FLUSH:
-      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "frame flush must be 0 or 1");
+      if (v < 0 || v > 2) return set_err(&c->err, CVR_ERR_INVALID, "frame flush must be 0, 1 or 2");
       c->frame_flush = (int)v;
       return CVR_OK;
     case CVR_OPT_DRAIN:
@@ -1701,6 +1701,7 @@ static int render_frame_flush(cvr_ctx* c, float* host_image, void* dhost, cvr_st
   hdr.status = dstatus;
   hdr.host_w = W;
   hdr.scale = (float)c->iterations;
+  hdr.give_up = c->frame_flush == 2 ? 1u : 0u;
   // the header only travels when it changed (the same host image frame after frame: none)
   const bool send_hdr = !c->flush_hdr_valid || memcmp(&hdr, &c->flush_hdr, sizeof(hdr)) != 0;
   c->flush_hdr = hdr;

@@ -256,7 +256,8 @@ struct FrameFlush {
                          // [kFrameFlushers] flushers that gave up waiting
   uint32_t host_w;       // host image row length in pixels
   float scale;           // the Scale functor's divisor (iterations)
-  uint32_t pad[10];
+  uint32_t give_up;      // test mode (CVR_OPT_FRAME_FLUSH 2): the flushers give up at once
+  uint32_t pad[9];
 };
 static_assert(sizeof(FrameFlush) == 64, "FrameFlush is the 64-byte header below frame_done");
 constexpr uint32_t kFrameFlushers = 8;  // the first workgroups of a flushing launch

@@ -110,7 +110,8 @@ typedef enum {
                                  host image: 1 (default) the launch itself stores each 8x8 block's
                                  normalised pixels into the host image once all its paths have
                                  ended (cvr_frame_flush_info); 0 normalise + copy after the launch.
-                                 Same image either way (C2: 5.21 vs 5.34 ms per call). */
+                                 Same image either way (C2: 5.14 vs 5.29 ms per call).  2 (tests):
+                                 the flushers give up at once, so the call takes its fallback copy. */
   /* 21: unused (a drain-time path migration between waves, measured slower: DESIGN.md §6) */
   CVR_OPT_DRAIN = 22,          /* wave-pool scheduler, once the queues are empty: an event batch runs as
                                  soon as the waiting segments x d >= the tracking ones (d = 0: only when

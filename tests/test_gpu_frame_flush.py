@@ -168,3 +168,33 @@ def test_flush_with_block_order_and_other_budgets(cvr):
     finally:
         buf.close()
         c.close()
+
+
+def test_flush_fallback_copy(cvr):
+    """CVR_OPT_FRAME_FLUSH 2 (test mode): the flushers give up at once and the
+    call copies the image after the launch instead; same image, the fallback
+    counted, and the next flushed frame works again."""
+    scene = _scene(cvr, "hetvol")
+    c, _, _ = _context(cvr, scene, 96, 64, 3)
+    buf = Pinned(96, 64)
+    try:
+        c.set_seed(1)
+        c.render_frame(buf.ptr.value, 1, stats=False)
+        assert c.frame_flush_info() == (96, 0)
+        ref = buf.img.copy()
+        c.set_option(cvr.OPT_FRAME_FLUSH, 2)
+        buf.img[:] = np.nan
+        c.set_seed(1)
+        _, st = c.render_frame(buf.ptr.value, 1)
+        assert c.frame_flush_info() == (0, 1)
+        assert st.paths == 96 * 64 * 3
+        assert np.array_equal(buf.img[..., 3], ref[..., 3])
+        assert_pixels_close(buf.img[..., :3], ref[..., :3], 3, "fallback")
+        c.set_option(cvr.OPT_FRAME_FLUSH, 1)
+        c.set_seed(1)
+        c.render_frame(buf.ptr.value, 1, stats=False)
+        assert c.frame_flush_info() == (96, 1)
+        assert_pixels_close(buf.img[..., :3], ref[..., :3], 3, "flush after fallback")
+    finally:
+        buf.close()
+        c.close()
