@@ -815,6 +815,57 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
       CVR_LAP(6)
 #endif
+      // A path's end of event: roulette death, or the AABB test of its next segment
+      // (escape: splat; else its slot is stored).
+#define CVR_FINISH_EVENT(ALIVE)                                                          \
+  if (!(ALIVE)) { /* the path died in roulette */                                     \
+    to_ln = true;                                                                        \
+    if (kFlush) S.meta[s] = ps.image_id; /* the ended path's pixel (in-launch output) */ \
+    if (kRecord) record_end<kSlots>(L, s, ps, 0u, nseg);                               \
+  } else if (L.max_segments && nseg >= L.max_segments) {                                 \
+    truncated = true;                                                                    \
+    to_ln = true;                                                                        \
+    if (kFlush) S.meta[s] = ps.image_id;                                                 \
+    if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);                               \
+  } else {                                                                               \
+    ++nseg;                                                                              \
+    seg_next = true;                                                                     \
+    if (!aabb_intersect(me, ps.o, ps.d, is)) {                                           \
+      splat(L, ps);                                                                      \
+      escaped = true;                                                                    \
+      to_ln = true;                                                                      \
+      if (kFlush) S.meta[s] = ps.image_id;                                               \
+      if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);                             \
+    } else {                                                                             \
+      store_full(S, gT, s, ps, is, nseg);                                                \
+      to_ready = is.inside; /* medium: Woodcock from t = 0 */                            \
+      to_lb = !is.inside;   /* no medium: boundary at isect.dist */                      \
+    }                                                                                    \
+  }
+#ifndef CVR_WPOOL_EARLY_FINISH
+#define CVR_WPOOL_EARLY_FINISH 0
+#endif
+#if CVR_WPOOL_EARLY_FINISH
+      // each kind's paths finish right after their part: the boundary part's stores and
+      // splats are then in flight while the collision part computes
+      if (kind == K_BOUNDARY) {
+        boundary_event(me, ps, is);
+        const bool alive = roulette(ps);
+        CVR_FINISH_EVENT(alive)
+      }
+#if CVR_STAMPS
+      CVR_LAP(7)
+#endif
+      if (kind == K_COLLIDE) {
+        scatter_event<kScatterEps>(me, ps, t_hit);
+        const bool alive = roulette(ps);
+        CVR_FINISH_EVENT(alive)
+      }
+#if CVR_STAMPS
+      CVR_LAP(8)
+#endif
+      const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
+#else
       bool alive = false;
       if (kind == K_BOUNDARY) {
         boundary_event(me, ps, is);
@@ -859,6 +910,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           }
         }
       }
+#endif
+#undef CVR_FINISH_EVENT
 #if CVR_STAMPS
       t_regen = __builtin_amdgcn_s_memtime();
 #endif
