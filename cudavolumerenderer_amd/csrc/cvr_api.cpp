@@ -71,6 +71,7 @@ struct cvr_ctx {
   float4* d_albedo = nullptr;
   float4* d_cells = nullptr;  // corner-replicated density (MediumParams::cells)
   bool use_cells = true;
+  bool uniform_albedo = true;  // CVR_OPT_UNIFORM_ALBEDO
   uint8_t* d_bounds = nullptr;  // brick bounds (MediumParams::bounds)
   uint32_t bound_shift = 2;     // log2 brick size, 0 = off
   bool bound_shift_set = false; // CVR_OPT_BOUNDS given (else sparse media use 8^3 bricks)
@@ -775,6 +776,15 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   m.albedo = c->d_albedo;
   fill_medium_common(m, md->res, md->box_min, md->box_max, md->scale, md->max_density, md->g, md->roughness,
                      md->eta);
+  if (c->uniform_albedo) {
+    // every voxel's rgb bit-identical to the first (the XML smoke scene's constant albedo)
+    bool same = true;
+    for (size_t i = 1; i < n && same; ++i) same = memcmp(md->albedo + 4 * i, md->albedo, 3 * sizeof(float)) == 0;
+    if (same) {
+      m.albedo_uniform = 1u;
+      m.albedo_bg = cvr::V3{md->albedo[0], md->albedo[1], md->albedo[2]};
+    }
+  }
   c->have_medium = true;
   return CVR_OK;
 }
@@ -1173,6 +1183,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
     case CVR_OPT_CELLS:
       // takes effect at the next cvr_set_medium
       c->use_cells = v != 0;
+      return CVR_OK;
+    case CVR_OPT_UNIFORM_ALBEDO:
+      // takes effect at the next cvr_set_medium
+      c->uniform_albedo = v != 0;
       return CVR_OK;
     case CVR_OPT_RNG_BINDING:
       if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "rng binding must be 0 (path) or 1 (thread)");

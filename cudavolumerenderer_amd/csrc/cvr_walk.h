@@ -149,6 +149,11 @@ struct MediumParams {
   uint32_t cnx, cnxy;                      // macros per x row / per xy plane
   uint32_t lnx, lny;                       // leaves per x / y row
   V3 albedo_bg;
+  // Dense media: every albedo voxel holds the same rgb (detected at cvr_set_medium,
+  // CVR_OPT_UNIFORM_ALBEDO), stored in albedo_bg: the 8 taps of a collision's albedo
+  // lookup are that constant, interpolated with the same operations, and nothing is
+  // loaded (the same values, so the same result).
+  uint32_t albedo_uniform;
   uint32_t rx, ry, rz;
   uint32_t rxy;                  // rx * ry (< 2^24 for a dense medium)
   float fres_x, fres_y, fres_z;  // (float)res
@@ -384,6 +389,7 @@ CVR_DEV float4 texel_albedo(const MediumParams& m, uint32_t x, uint32_t y, uint3
     return slot == 0xFFFFFFFFu ? make_float4(m.albedo_bg.x, m.albedo_bg.y, m.albedo_bg.z, 1.0f)
                                : m.leaf_albedo[((size_t)slot << 9) | leaf_local(x, y, z)];
   }
+  if (m.albedo_uniform) return make_float4(m.albedo_bg.x, m.albedo_bg.y, m.albedo_bg.z, 1.0f);
   return m.albedo[(z * m.ry + y) * m.rx + x];
 }
 

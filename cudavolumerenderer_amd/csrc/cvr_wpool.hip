@@ -629,6 +629,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     me.bmin = mk3(opaque_s(m.bmin.x), opaque_s(m.bmin.y), opaque_s(m.bmin.z));
     me.bmax = mk3(opaque_s(m.bmax.x), opaque_s(m.bmax.y), opaque_s(m.bmax.z));
     me.albedo_bg = mk3(opaque_s(m.albedo_bg.x), opaque_s(m.albedo_bg.y), opaque_s(m.albedo_bg.z));
+    me.albedo_uniform = __float_as_uint(opaque_s(__uint_as_float(m.albedo_uniform)));
     // One batch of up to 64 items, [boundary | collision | new].  New items
     // are regenerated first: a camera path's first segment is an AABB test
     // and, when it hits the box from outside, a boundary event, which then

@@ -106,6 +106,10 @@ typedef enum {
                                  paths per wave of the occupancy grid half of it (a quarter with renders
                                  in flight), below 1024 paths per wave half of it with renders in flight,
                                  else all of it.  Scheduling only. */
+  CVR_OPT_UNIFORM_ALBEDO = 25, /* dense media: 1 (default) a grid whose voxels all hold the same rgb is
+                                 read as that constant (the 8 taps interpolated with the same
+                                 operations, no loads: the same result); 0 always load.  Takes
+                                 effect at the next cvr_set_medium. */
   CVR_OPT_FRAME_FLUSH = 24,    /* cvr_render_frame, one part, wave-pool scheduler, pinned or registered
                                  host image: 1 (default) the launch itself stores each 8x8 block's
                                  normalised pixels into the host image once all its paths have

@@ -63,6 +63,8 @@ def main():
         k, d = parse(v)
         c = cvr.Context(0, k)
         c.set_option(cvr.OPT_CELLS, d.get("cells", 1))
+        if "ualb" in d:
+            c.set_option(cvr.OPT_UNIFORM_ALBEDO, d["ualb"])
         if "bounds" in d:
             c.set_option(cvr.OPT_BOUNDS, d["bounds"])
         if scene.is_sparse or d.get("sparse", 0):
