@@ -149,11 +149,6 @@ struct MediumParams {
   uint32_t cnx, cnxy;                      // macros per x row / per xy plane
   uint32_t lnx, lny;                       // leaves per x / y row
   V3 albedo_bg;
-  // Dense media: every albedo voxel holds the same rgb (detected at cvr_set_medium,
-  // CVR_OPT_UNIFORM_ALBEDO), stored in albedo_bg: the 8 taps of a collision's albedo
-  // lookup are that constant, interpolated with the same operations, and nothing is
-  // loaded (the same values, so the same result).
-  uint32_t albedo_uniform;
   uint32_t rx, ry, rz;
   uint32_t rxy;                  // rx * ry (< 2^24 for a dense medium)
   float fres_x, fres_y, fres_z;  // (float)res
@@ -172,6 +167,12 @@ struct MediumParams {
   float ax, ay;      // GGX roughness
   float eta;         // int_ior / ext_ior
   float inv_eta;     // 1.0f / eta
+  // Dense media: every albedo voxel holds the same rgb (detected at cvr_set_medium,
+  // CVR_OPT_UNIFORM_ALBEDO), stored in albedo_bg: the 8 taps of a collision's albedo
+  // lookup are that constant, interpolated with the same operations, and nothing is
+  // loaded (the same values, so the same result).  Last, so that the other fields
+  // keep their kernel-argument offsets.
+  uint32_t albedo_uniform;
 };
 
 // 1: sparse media bound their Woodcock points with macro words first (see

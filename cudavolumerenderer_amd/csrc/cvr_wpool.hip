@@ -403,10 +403,12 @@ __device__ void frame_flusher(const LaunchParams& L) {
 
 // kMed: the medium layout the instance is compiled for (kMedDense any dense medium,
 // kMedSparse leaves + brick words, kMedDenseFull a dense medium with density cells
-// and brick bounds, the defaults: its null checks fold away, C2 -0.6%, C3 -1.8%).
+// and brick bounds, the defaults: its null checks fold away, C2 -0.6%, C3 -1.8%;
+// kMedDenseFullUniform the same with a uniform albedo, MediumParams::albedo_uniform,
+// whose check would otherwise cost the non-uniform instance 1.5% on C2).
 // kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
 // the other instances carry none of its code.
-enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2 };
+enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2, kMedDenseFullUniform = 3 };
 template <bool kScatterEps, int kWaves, int kMed, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr bool kSparse = kMed == kMedSparse;
@@ -427,9 +429,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
     m.scoarse = nullptr;
-    if constexpr (kMed == kMedDenseFull) {
+    if constexpr (kMed == kMedDenseFull || kMed == kMedDenseFullUniform) {
       __builtin_assume(m.cells != nullptr);
       __builtin_assume(m.bounds != nullptr);
+      m.albedo_uniform = kMed == kMedDenseFullUniform ? 1u : 0u;
     }
   } else if (CVR_SPARSE_SPECIALISE) {
     // and sparse instances see the dense pointers as constant null (a sparse medium
@@ -440,6 +443,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     __builtin_assume(m.leaves != nullptr);
     __builtin_assume(m.sbounds != nullptr);
     if (!CVR_SPARSE_2LEVEL) m.scoarse = nullptr;
+    m.albedo_uniform = 0u;
   }
   static_assert(sizeof(WavePool<kSlots, kSplit>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves, kSplit>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
@@ -629,7 +633,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     me.bmin = mk3(opaque_s(m.bmin.x), opaque_s(m.bmin.y), opaque_s(m.bmin.z));
     me.bmax = mk3(opaque_s(m.bmax.x), opaque_s(m.bmax.y), opaque_s(m.bmax.z));
     me.albedo_bg = mk3(opaque_s(m.albedo_bg.x), opaque_s(m.albedo_bg.y), opaque_s(m.albedo_bg.z));
-    me.albedo_uniform = __float_as_uint(opaque_s(__uint_as_float(m.albedo_uniform)));
+    if constexpr (kMed == kMedDense)  // a run-time flag only in the generic instance
+      me.albedo_uniform = __float_as_uint(opaque_s(__uint_as_float(m.albedo_uniform)));
     // One batch of up to 64 items, [boundary | collision | new].  New items
     // are regenerated first: a camera path's first segment is an AABB test
     // and, when it hits the box from outside, a boundary event, which then
@@ -1031,10 +1036,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 // Instances: 5 waves per SIMD (the default budget) for every medium layout, with and
 // without the in-launch output; the other budgets for the generic layouts.
 template <bool E>
-static const void* wpool_fn(int waves, bool sparse, bool full, bool flush = false) {
+static const void* wpool_fn(int waves, bool sparse, bool full, bool flush = false, bool uniform = false) {
 #define CVR_WP(W, M, F) reinterpret_cast<const void*>(&k_wpool<E, W, M, false, F>)
   if (waves == 5) {
     if (sparse) return flush ? CVR_WP(5, kMedSparse, true) : CVR_WP(5, kMedSparse, false);
+    if (full && uniform) return flush ? CVR_WP(5, kMedDenseFullUniform, true) : CVR_WP(5, kMedDenseFullUniform, false);
     if (full) return flush ? CVR_WP(5, kMedDenseFull, true) : CVR_WP(5, kMedDenseFull, false);
     return flush ? CVR_WP(5, kMedDense, true) : CVR_WP(5, kMedDense, false);
   }
@@ -1061,9 +1067,11 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   const bool sparse = m.leaves != nullptr;
   const bool flush = L.frame_done != nullptr;
   const bool full = !sparse && m.cells != nullptr && m.bounds != nullptr;
+  const bool uniform = m.albedo_uniform != 0u;
   if (L.rec && flush) return hipErrorInvalidValue;
   const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
-                         : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush) : wpool_fn<false>(waves, sparse, full, flush));
+                         : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush, uniform)
+                                        : wpool_fn<false>(waves, sparse, full, flush, uniform));
   if (!fn) return hipErrorInvalidValue;  // no record / in-launch output instance for this register budget
   MediumParams mm = m;
   LaunchParams ll = L;
