@@ -1691,7 +1691,7 @@ static void copy_settings(cvr_ctx* d, const cvr_ctx* s) {
 // cvr_render_frame with the in-launch output: the clear, the header and the block
 // counts, one launch whose flusher waves store the normalised blocks into the host
 // image (device address dhost), and the copy after the launch only if a flusher gave up.
-static int render_frame_flush(cvr_ctx* c, float* host_image, void* dhost, cvr_stats* stats) {
+static int render_frame_flush(cvr_ctx* c, void* dhost, cvr_stats* stats) {
   const uint32_t W = c->tile_w, H = c->tile_h;
   const size_t px = (size_t)W * H, nb = (size_t)(W / 8u) * (H / 8u);
   if (c->flush_blocks < nb) {
@@ -1746,7 +1746,6 @@ static int render_frame_flush(cvr_ctx* c, float* host_image, void* dhost, cvr_st
   } else {
     c->flush_last_blocks = (uint32_t)stored;
   }
-  (void)host_image;
   c->seed = seed_after_resets(c, c->seed, 1);  // reset(): prepareForNextIterations
   if (!stats) return CVR_OK;
   cvr_stats acc{};
@@ -1806,7 +1805,7 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* s
       dhost = nullptr;
     }
   }
-  if (dhost) return render_frame_flush(c, host_image, dhost, stats);
+  if (dhost) return render_frame_flush(c, dhost, stats);
   c->flush_last_blocks = 0;
   while (c->frame_kids.size() + 1 < parts) {
     cvr_ctx* k = nullptr;
