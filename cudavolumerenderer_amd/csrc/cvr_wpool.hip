@@ -409,8 +409,20 @@ __device__ void frame_flusher(const LaunchParams& L) {
 // kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
 // the other instances carry none of its code.
 enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2, kMedDenseFullUniform = 3 };
+// Deferred splats (experiment, not kFlush, whose block counts assume a batch's splats
+// are issued in it): a batch's escapes are splatted by the next batch, so the track
+// loop's first load after a batch does not wait for that batch's framebuffer atomics
+// (gfx950 counts stores and atomics in vmcnt with the loads).  1: at the next batch's
+// start, 2: after its slot loads, 3: after its event parts.
+#ifndef CVR_WPOOL_DEFER_SPLAT
+#define CVR_WPOOL_DEFER_SPLAT 0
+#endif
+#if CVR_WPOOL_DEFER_SPLAT && CVR_WPOOL_EARLY_FINISH
+#error "deferred splats are not built for the early-finish variant"
+#endif
 template <bool kScatterEps, int kWaves, int kMed, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
+  constexpr bool kDeferSplat = CVR_WPOOL_DEFER_SPLAT != 0 && !kFlush;
   constexpr bool kSparse = kMed == kMedSparse;
   constexpr bool kSplit = !kSparse || CVR_WPOOL_SPLIT_SPARSE;
   constexpr int kSlots = PoolSize<kWaves, kSplit>::value;
@@ -608,6 +620,26 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
     // ================================================= EVENT ==============
     __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
+    // Deferred splats (kDeferSplat): the last batch's escapes, parked in their free slots'
+    // a[] (T, image_id) and filed first on the ln stack, read before this batch's
+    // regeneration can reuse those slots, and issued after this batch's slot loads.
+    float4 dsp = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    bool dlive = false;
+    if constexpr (kDeferSplat) {
+      const uint32_t pd = S.pend;
+      if (lane < (pd >> 8)) {
+        dsp = S.a[S.ln[(pd & 0xFFu) + lane]];
+        dlive = true;
+      }
+    }
+#define CVR_DEFERRED_SPLAT()                 \
+  if (dlive) {                               \
+    PathState q{};                           \
+    q.T = mk3(dsp.x, dsp.y, dsp.z);          \
+    q.image_id = __float_as_uint(dsp.w);     \
+    splat(L, q);                             \
+  }
+    if constexpr (kDeferSplat && CVR_WPOOL_DEFER_SPLAT == 1) { CVR_DEFERRED_SPLAT() }
     if constexpr (kFlush) {
       const uint32_t pend = S.pend;  // the last batch's ended paths (in-launch output)
       if (!(CVR_DIAG_COUNT & 4) && pend != 0u) {
@@ -797,7 +829,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             ++nseg;
             seg_first = true;
             if (!aabb_intersect(me, ps.o, ps.d, is)) {
-              splat(L, ps);
+              if constexpr (kDeferSplat) S.a[s] = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
+              else splat(L, ps);
               escaped = true;
               to_ln = true;
               if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
@@ -818,6 +851,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       if (lane < tb + tc) load_full(S, gT, s, ps, is, nseg, t_hit);
       // a filed boundary whose last step passed max_t drew one number too many
       if (lane < tb && !(t_hit <= is.dist)) rng_undo(ps.rng);
+      if constexpr (kDeferSplat && CVR_WPOOL_DEFER_SPLAT == 2) { CVR_DEFERRED_SPLAT() }
 #if CVR_STAMPS
       CVR_LAP(6)
 #endif
@@ -887,6 +921,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #if CVR_STAMPS
       CVR_LAP(8)
 #endif
+      if constexpr (kDeferSplat && CVR_WPOOL_DEFER_SPLAT == 3) { CVR_DEFERRED_SPLAT() }
       const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
       if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {  // the path died in roulette
         to_ln = true;
@@ -904,7 +939,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           ++nseg;
           seg_next = true;
           if (!aabb_intersect(me, ps.o, ps.d, is)) {
-            splat(L, ps);
+            if constexpr (kDeferSplat) S.a[s] = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
+            else splat(L, ps);
             escaped = true;
             to_ln = true;
             if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
@@ -936,7 +972,15 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       const unsigned long long mr = __ballot(to_ready), mb = __ballot(to_lb), mn = __ballot(to_ln);
       if (to_ready) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)s;
       if (to_lb) S.lb[n_lb + lane_rank(mb)] = (uint8_t)s;
-      if (to_ln) S.ln[n_ln + lane_rank(mn)] = (uint8_t)s;
+      if constexpr (kDeferSplat) {
+        // escapes first on the ln stack: the next batch splats ln[n_ln, + their count)
+        const unsigned long long mx = __ballot(escaped);
+        const uint32_t n_x = (uint32_t)__popcll(mx);
+        if (to_ln) S.ln[n_ln + (escaped ? lane_rank(mx) : n_x + lane_rank(mn & ~mx))] = (uint8_t)s;
+        if (lane == 0) S.pend = n_x != 0u ? n_ln | n_x << 8 : 0u;
+      } else if (to_ln) {
+        S.ln[n_ln + lane_rank(mn)] = (uint8_t)s;
+      }
       if constexpr (kFlush) {
         // in-launch output: the ended paths (their slots' meta holds the pixel) are counted
         // at the next batch
@@ -991,6 +1035,17 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #endif
   }
 
+  if constexpr (kDeferSplat) {  // the last batch's escapes
+    const uint32_t pd = S.pend;
+    if (lane < (pd >> 8)) {
+      const float4 f = S.a[S.ln[(pd & 0xFFu) + lane]];
+      PathState q{};
+      q.T = mk3(f.x, f.y, f.z);
+      q.image_id = __float_as_uint(f.w);
+      splat(L, q);
+    }
+  }
+#undef CVR_DEFERRED_SPLAT
   if constexpr (kFlush) {
     const uint32_t pend = S.pend;  // raw: the last batch's ended paths
     if (pend != 0u) {
