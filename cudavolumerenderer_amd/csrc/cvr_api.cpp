@@ -183,14 +183,11 @@ struct cvr_ctx {
   uint32_t flush_last_blocks = 0, flush_fallbacks = 0;
 };
 
-#ifndef CVR_TAILSTAMPS
-#define CVR_TAILSTAMPS 0
-#endif
 using cvr::kWorkDebug;
 using cvr::kWorkQueues;
 using cvr::kWorkStats;
 // d_work layout: cvr_kernels.h (stats, debug counters, queue heads)
-constexpr size_t kWorkBytes = cvr::kWorkBytesBase + (CVR_TAILSTAMPS ? (size_t)(80 + 384) * 65536 : 0);
+constexpr size_t kWorkBytes = cvr::kWorkBytesBase;
 
 #define HIP_TRY(ctx, expr)                                                                         \
   do {                                                                                                  \
@@ -1459,21 +1456,6 @@ int cvr_debug_counters(cvr_ctx* c, uint64_t out[16]) {
   return CVR_OK;
 }
 
-#if CVR_TAILSTAMPS
-// Diagnostic build only: the wave pool's per-wave stamps (10 u64 per wave, cvr_wpool.hip).
-int cvr_debug_tailstamps(cvr_ctx* c, uint64_t* out, size_t n_waves) {
-  if (!c || !out || n_waves > 65536) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "bad argument");
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
-  HIP_TRY(c, hipMemcpy(out, c->d_work + cvr::kWorkBytesBase, n_waves * 80, hipMemcpyDeviceToHost));
-  return CVR_OK;
-}
-// the drain timelines (48 u64 per wave) that follow the stamps of the launch's `grid` waves
-int cvr_debug_tailtimeline(cvr_ctx* c, uint64_t* out, size_t grid) {
-  if (!c || !out || grid > 65536) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "bad argument");
-  HIP_TRY(c, hipMemcpy(out, c->d_work + cvr::kWorkBytesBase + grid * 80, grid * 48 * 8, hipMemcpyDeviceToHost));
-  return CVR_OK;
-}
-#endif
 
 int cvr_copy_output(cvr_ctx* c, float* host, float scale) {
   if (!c || !host) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");

@@ -10,11 +10,9 @@ namespace cvr {
 
 // Per-context work area (cvr_api.cpp d_work, zeroed per launch), in bytes:
 // 16 u64 stats at 0, 16 u64 diagnostic counters at 128, up to 64 queue heads
-// from 256 (one 64-byte line each, LaunchParams::queue), and in diagnostic
-// builds (CVR_TAILSTAMPS) per-wave stamps from kWorkBytesBase.
+// from 256 (one 64-byte line each, LaunchParams::queue).
 constexpr size_t kWorkStats = 0, kWorkDebug = 128, kWorkQueues = 256, kMaxQueues = 64;
 constexpr size_t kWorkBytesBase = kWorkQueues + kMaxQueues * 64;
-constexpr uint32_t kStampWord = (uint32_t)(kWorkBytesBase / 8);  // in L.stats words
 
 // Per-path debug record; layout identical to cvr_path_record (include/cvr.h)
 // and oracle_path (oracle/cvr_oracle.c).

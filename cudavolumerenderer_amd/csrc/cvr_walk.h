@@ -269,10 +269,7 @@ static_assert(sizeof(FrameFlush) == 64, "FrameFlush is the 64-byte header below 
 constexpr uint32_t kFrameFlushers = 8;  // the first workgroups of a flushing launch
 // one count per 64-byte line: blocks dequeued together are counted by different
 // waves at the same time, and atomics on one line serialise at the memory side
-#ifndef CVR_DONE_STRIDE
-#define CVR_DONE_STRIDE 16
-#endif
-constexpr uint32_t kDoneStride = CVR_DONE_STRIDE;
+constexpr uint32_t kDoneStride = 16;
 CVR_DEV const FrameFlush* frame_header(const unsigned int* done) {
   return reinterpret_cast<const FrameFlush*>(done) - 1;
 }
@@ -835,53 +832,22 @@ CVR_DEV bool roulette(PathState& ps) {
   return true;
 }
 // atomicVectorAdd (Utilities.cuh:15-22) with Le = 1.
-#ifndef CVR_DIAG_NO_SPLAT  // diagnostic builds only (tools/job_writes.sh): no framebuffer writes
-#define CVR_DIAG_NO_SPLAT 0
-#endif
-#ifndef CVR_DIAG_SPLAT_WG  // diagnostic builds only: workgroup-scope splat atomics (timing experiment)
-#define CVR_DIAG_SPLAT_WG 0
-#endif
-#ifndef CVR_SPLAT_SKIP_ZERO
-#define CVR_SPLAT_SKIP_ZERO 1
-#endif
 CVR_DEV void splat(const LaunchParams& L, const PathState& ps) {
-  if (CVR_DIAG_NO_SPLAT == 1) return;
   gptr_t<float> px = gmem(reinterpret_cast<float*>(L.out + ps.image_id));
-  if (CVR_DIAG_NO_SPLAT == 2) {  // diagnostic: the w store only
-    px[3] = 1.0f;
-    return;
-  }
-  if (CVR_DIAG_SPLAT_WG) {
-    __hip_atomic_fetch_add(px + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(px + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __hip_atomic_fetch_add(px + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  } else if (CVR_SPLAT_SKIP_ZERO) {
-    // A zero component is not added: a pixel is never -0 (cleared to +0, and every
-    // contribution is >= +0 or NaN: albedo and G1 factors are >= 0, roulette divides by
-    // p > 0), so x + 0 == x and the sum is the same.  After one collision in a medium
-    // with albedo (d, 0, 0) (the MHD converter's, mhd_to_vdb.py:62-64) two of the
-    // three atomics go.
-    if (ps.T.x != 0.0f) __hip_atomic_fetch_add(px + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ps.T.y != 0.0f) __hip_atomic_fetch_add(px + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ps.T.z != 0.0f) __hip_atomic_fetch_add(px + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    __hip_atomic_fetch_add(px + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(px + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(px + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-// w = 1 (Utilities.cuh:21, a plain store there) as a memory-side atomic swap: a plain
-// store leaves the pixel's line dirty in this XCD's L2 while the rgb atomics are
-// performed at the memory side, and the mix cost C2 1.3% and C3 1.5% of kernel time
-// (profiles/round3/ab/splat_w/).  Same value, same image.
-#ifndef CVR_SPLAT_W_ATOMIC
-#define CVR_SPLAT_W_ATOMIC 1
-#endif
-  if (CVR_DIAG_NO_SPLAT == 3) return;  // diagnostic 3: the atomics only
-  if (CVR_SPLAT_W_ATOMIC)
-    (void)__hip_atomic_exchange(reinterpret_cast<gptr_t<unsigned int>>(px + 3), 0x3F800000u, __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-  else
-    px[3] = 1.0f;
+  // A zero component is not added: a pixel is never -0 (cleared to +0, and every
+  // contribution is >= +0 or NaN: albedo and G1 factors are >= 0, roulette divides by
+  // p > 0), so x + 0 == x and the sum is the same.  After one collision in a medium
+  // with albedo (d, 0, 0) (the MHD converter's, mhd_to_vdb.py:62-64) two of the
+  // three atomics go.
+  if (ps.T.x != 0.0f) __hip_atomic_fetch_add(px + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ps.T.y != 0.0f) __hip_atomic_fetch_add(px + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ps.T.z != 0.0f) __hip_atomic_fetch_add(px + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // w = 1 (Utilities.cuh:21, a plain store there) as a memory-side atomic swap: a plain
+  // store leaves the pixel's line dirty in this XCD's L2 while the rgb atomics are
+  // performed at the memory side, and the mix cost C2 1.3% and C3 1.5% of kernel time
+  // (profiles/round3/ab/splat_w/).  Same value, same image.
+  (void)__hip_atomic_exchange(reinterpret_cast<gptr_t<unsigned int>>(px + 3), 0x3F800000u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------ naiveMK -----

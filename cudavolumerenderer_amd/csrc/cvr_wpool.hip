@@ -28,14 +28,6 @@
 #include "cvr_kernels.h"
 #include "cvr_walk.h"
 
-#ifndef CVR_STAMPS
-#define CVR_STAMPS 0
-#endif
-// Diagnostic build (tools/tailstamps.py): per-wave wall-clock stamps of the
-// launch's ramp-up and drain, written after the stats words.
-#ifndef CVR_TAILSTAMPS
-#define CVR_TAILSTAMPS 0
-#endif
 // Woodcock steps per track iteration between swap/event checks.
 #ifndef CVR_WPOOL_UNROLL
 #define CVR_WPOOL_UNROLL 4
@@ -43,12 +35,7 @@
 // Wave priorities (s_setprio): the track loop above the event code, so a
 // stepping wave issues its brick-bound and cell loads ahead of the
 // VALU-dense event batches of the other waves on its SIMD (C2: -0.7%).
-#ifndef CVR_PRIO_TRACK
-#define CVR_PRIO_TRACK 1
-#endif
-#ifndef CVR_PRIO_EVENT
-#define CVR_PRIO_EVENT 0
-#endif
+constexpr int kPrioTrack = 1, kPrioEvent = 0;
 
 namespace cvr {
 
@@ -74,31 +61,19 @@ __device__ __forceinline__ float opaque_s(float x) {
 // one-wave workgroups of 7680 B fit 20 per CU, of 7936 / 8064 / 8192 B only 18,
 // although the occupancy API answers 20 for all of them; 10240 B fit 16).  A
 // budget of 163840 / 20 = 8192 B therefore ran 4.5 waves per SIMD, not 5.
-#ifndef CVR_LDS_GRANULE
-#define CVR_LDS_GRANULE 1280
-#endif
-template <int kWaves, bool kSplit>
+constexpr int kLdsGranule = 1280;
+template <int kWaves>
 struct PoolSize {
   // LDS bytes per one-wave workgroup
-  static constexpr int kBudget = 163840 / (4 * kWaves) / CVR_LDS_GRANULE * CVR_LDS_GRANULE;
+  static constexpr int kBudget = 163840 / (4 * kWaves) / kLdsGranule * kLdsGranule;
   static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
-#ifdef CVR_WPOOL_SLOTS  // experiment builds: a smaller pool
-  static constexpr int value = CVR_WPOOL_SLOTS;
-#else
-  static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT) / (kSplit ? 64 : 80);
+  static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT) / 64;
   static_assert(4 * STAT_COUNT + 8 + 12 + 4 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
-#endif
 };
 // Sparse media (C5) split the slot too and run 5 waves per SIMD: 142.7 ms vs
 // 147.6 with the event part in LDS at 4 waves (round 3, once the global part's
 // loads and stores stopped being flat instructions that LDS waits also waited
 // for; round 2 measured 156.8 split at 4 waves, 153.7 at 5).
-#ifndef CVR_SPARSE_SPECIALISE
-#define CVR_SPARSE_SPECIALISE 1
-#endif
-#ifndef CVR_WPOOL_SPLIT_SPARSE
-#define CVR_WPOOL_SPLIT_SPARSE 1
-#endif
 
 // One path per slot.  LDS holds what the track loop and the event code both
 // need, as arrays of 16-byte blocks (ds_read_b128 / ds_write_b128):
@@ -108,12 +83,11 @@ struct PoolSize {
 // (L.pool_T, one float4 per slot of every wave: ~10 MB, L2-resident), read
 // and written once per event; so a slot takes 64 LDS bytes instead of 84 and
 // the pool holds 30% more paths, enough for 5 waves per SIMD (C2: 5.25 ms
-// vs 5.40 at 4 waves with the whole slot in LDS).  !kSplit: f in LDS.
-template <int kSlots, bool kSplit>
+// vs 5.40 at 4 waves with the whole slot in LDS).
+template <int kSlots>
 struct WavePool {
   float4 a[kSlots], b[kSlots];
   uint4 c[kSlots];
-  float4 f[kSplit ? 0 : kSlots];  // (T, image_id) when not split (none when split)
   uint2 e[kSlots];
   uint32_t meta[kSlots];
   uint8_t ready[kSlots];   // ring of track-ready slots
@@ -145,22 +119,20 @@ __device__ __forceinline__ V3 normal_of(uint32_t c) {
   return c == 0u ? mk3(0, 0, 0) : c <= 2u ? mk3(s, 0, 0) : c <= 4u ? mk3(0, s, 0) : mk3(0, 0, s);
 }
 
-template <int kSlots, bool kSplit>
-__device__ __forceinline__ void store_full(WavePool<kSlots, kSplit>& S, float4* __restrict__ gT, uint32_t s,
+template <int kSlots>
+__device__ __forceinline__ void store_full(WavePool<kSlots>& S, float4* __restrict__ gT, uint32_t s,
                                            const PathState& ps, const Isect& is, uint32_t nseg) {
   S.a[s] = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
   S.b[s] = make_float4(ps.d.x, ps.d.y, ps.d.z, is.dist);
   S.c[s] = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);
   S.e[s] = make_uint2(ps.rng.v4, ps.rng.d);
   S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
-  const float4 f = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
-  if constexpr (kSplit) gstore4(gT + s, f);
-  else S.f[s] = f;
+  gstore4(gT + s, make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id)));
 }
-template <int kSlots, bool kSplit>
-__device__ __forceinline__ void load_full(const WavePool<kSlots, kSplit>& S, const float4* __restrict__ gT, uint32_t s,
+template <int kSlots>
+__device__ __forceinline__ void load_full(const WavePool<kSlots>& S, const float4* __restrict__ gT, uint32_t s,
                                           PathState& ps, Isect& is, uint32_t& nseg, float& t) {
-  const float4 f = kSplit ? gload4(gT + s) : S.f[s];
+  const float4 f = gload4(gT + s);
   const float4 a = S.a[s], b = S.b[s];
   const uint4 c = S.c[s];
   const uint2 e = S.e[s];
@@ -176,15 +148,15 @@ __device__ __forceinline__ void load_full(const WavePool<kSlots, kSplit>& S, con
   is.inside = (meta & 8u) != 0u;
   nseg = meta >> 4;
 }
-template <int kSlots, bool kSplit>
-__device__ __forceinline__ void store_track(WavePool<kSlots, kSplit>& S, uint32_t s, float t, const Rng& rng) {
+template <int kSlots>
+__device__ __forceinline__ void store_track(WavePool<kSlots>& S, uint32_t s, float t, const Rng& rng) {
   S.a[s].w = t;
   S.c[s] = make_uint4(rng.v0, rng.v1, rng.v2, rng.v3);
   S.e[s] = make_uint2(rng.v4, rng.d);
 }
 // Track state of a ready path: o, t, d, max_t, rng.
-template <int kSlots, bool kSplit>
-__device__ __forceinline__ void load_track(const WavePool<kSlots, kSplit>& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
+template <int kSlots>
+__device__ __forceinline__ void load_track(const WavePool<kSlots>& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
                                            float& max_t) {
   const float4 a = S.a[s], b = S.b[s];
   const uint4 c = S.c[s];
@@ -252,39 +224,29 @@ __device__ __forceinline__ const LaunchParams& fresh(const LaunchParams& L) {
 constexpr unsigned kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 constexpr uint32_t kPendAgg = 0x80000000u;  // S.pend holds kPendAgg | block << 7 | count
 
-template <int kSlots, bool kSplit>
-__device__ __forceinline__ uint32_t count_ended(const WavePool<kSlots, kSplit>& S, const LaunchParams& L, uint32_t pend,
+template <int kSlots>
+__device__ __forceinline__ uint32_t count_ended(const WavePool<kSlots>& S, const LaunchParams& L, uint32_t pend,
                                                 uint32_t lane) {
   const uint32_t base = pend & 0xFFu, n = pend >> 8;
-#ifndef CVR_DIAG_COUNT  // diagnostic builds: bit 0 no wait, bit 1 no atomics, bit 2 no counting
-#define CVR_DIAG_COUNT 0
-#endif
-  if (!(CVR_DIAG_COUNT & 1)) __builtin_amdgcn_s_waitcnt(kWaitVm0);
+  __builtin_amdgcn_s_waitcnt(kWaitVm0);
   uint32_t blk = 0;
   if (lane < n) blk = tile_block_of(fresh(L), S.meta[S.ln[base + lane]]);
   const uint32_t b0 = __builtin_amdgcn_readfirstlane(blk);
   const unsigned long long same = __ballot(lane < n && blk == b0);
-#ifndef CVR_COUNT_AGG2
-#define CVR_COUNT_AGG2 1
-#endif
+  // a second block (the wave's previous chunk) with one atomic too, the rest one per lane
   const bool rest = lane < n && blk != b0;
-  if (CVR_COUNT_AGG2) {  // a second block (the wave's previous chunk) with one atomic too
-    const unsigned long long rm = __ballot(rest);
-    if (rm != 0ull) {
-      const uint32_t first = (uint32_t)__builtin_ctzll(rm);
-      const uint32_t b1 = __builtin_amdgcn_readlane(blk, first);
-      const unsigned long long s1 = __ballot(rest && blk == b1);
-      if (!(CVR_DIAG_COUNT & 2) && (lane == first || (rest && blk != b1)))
-        __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * blk), lane == first ? (unsigned int)__popcll(s1) : 1u,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  } else if (!(CVR_DIAG_COUNT & 2) && rest) {
-    __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * blk), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long rm = __ballot(rest);
+  if (rm != 0ull) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(rm);
+    const uint32_t b1 = __builtin_amdgcn_readlane(blk, first);
+    const unsigned long long s1 = __ballot(rest && blk == b1);
+    if (lane == first || (rest && blk != b1))
+      __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * blk), lane == first ? (unsigned int)__popcll(s1) : 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   return kPendAgg | b0 << 7 | (uint32_t)__popcll(same);
 }
 __device__ __forceinline__ void add_counted(const LaunchParams& L, uint32_t agg) {
-  if (CVR_DIAG_COUNT & 2) return;
   __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * ((agg & ~kPendAgg) >> 7)), agg & 0x7Fu,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -335,11 +297,7 @@ __device__ __forceinline__ void store_blocks(const LaunchParams& L, const FrameF
 // copies the image after the launch.
 constexpr unsigned long long kFlushPatience = 100000000ull;  // s_memrealtime ticks (100 MHz)
 constexpr unsigned int kFlushed = 0x80000000u;
-#ifndef CVR_DIAG_FLUSH  // diagnostic builds: 1 = flushers store nothing (the host copies after the launch)
-#define CVR_DIAG_FLUSH 0
-#endif
 __device__ void frame_flusher(const LaunchParams& L) {
-  if (CVR_DIAG_FLUSH == 1) return;
   const FrameFlush F = *frame_header(L.frame_done);
   const uint32_t lane = threadIdx.x, f = blockIdx.x;
   if (F.give_up) {  // test mode: exercise the host's fallback copy
@@ -409,23 +367,10 @@ __device__ void frame_flusher(const LaunchParams& L) {
 // kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
 // the other instances carry none of its code.
 enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2, kMedDenseFullUniform = 3 };
-// Deferred splats (experiment, not kFlush, whose block counts assume a batch's splats
-// are issued in it): a batch's escapes are splatted by the next batch, so the track
-// loop's first load after a batch does not wait for that batch's framebuffer atomics
-// (gfx950 counts stores and atomics in vmcnt with the loads).  1: at the next batch's
-// start, 2: after its slot loads, 3: after its event parts.
-#ifndef CVR_WPOOL_DEFER_SPLAT
-#define CVR_WPOOL_DEFER_SPLAT 0
-#endif
-#if CVR_WPOOL_DEFER_SPLAT && CVR_WPOOL_EARLY_FINISH
-#error "deferred splats are not built for the early-finish variant"
-#endif
 template <bool kScatterEps, int kWaves, int kMed, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
-  constexpr bool kDeferSplat = CVR_WPOOL_DEFER_SPLAT != 0 && !kFlush;
   constexpr bool kSparse = kMed == kMedSparse;
-  constexpr bool kSplit = !kSparse || CVR_WPOOL_SPLIT_SPARSE;
-  constexpr int kSlots = PoolSize<kWaves, kSplit>::value;
+  constexpr int kSlots = PoolSize<kWaves>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
   // branches of the walk code fold away and take no scalar registers.
   if constexpr (kFlush) {
@@ -446,7 +391,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       __builtin_assume(m.bounds != nullptr);
       m.albedo_uniform = kMed == kMedDenseFullUniform ? 1u : 0u;
     }
-  } else if (CVR_SPARSE_SPECIALISE) {
+  } else {
     // and sparse instances see the dense pointers as constant null (a sparse medium
     // has leaves, brick words and no dense grids; two-level bounds are a build option)
     m.density = nullptr;
@@ -457,10 +402,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     if (!CVR_SPARSE_2LEVEL) m.scoarse = nullptr;
     m.albedo_uniform = 0u;
   }
-  static_assert(sizeof(WavePool<kSlots, kSplit>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves, kSplit>::kBudget,
+  static_assert(sizeof(WavePool<kSlots>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
   static_assert(kSlots <= 256, "the pool's rings and stacks hold slot indices as uint8_t");
-  __shared__ WavePool<kSlots, kSplit> S;
+  __shared__ WavePool<kSlots> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
   // scalars (v_readlane reloads in every Woodcock step).
@@ -491,34 +436,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   uint32_t ready_head = 0, n_ready = 0, n_lb = 0, n_lc = 0;
   uint32_t n_ln = kSlots;  // slots waiting for a new path (all of them at the start)
   for (uint32_t i = lane; i < (uint32_t)kSlots; i += 64u) S.ln[i] = (uint8_t)i;
-#if CVR_STAMPS
-  // event cycles, track cycles, event batches, track iterations, event-code cycles, regen+AABB cycles,
-  // load, boundary, collision, regeneration cycles
-  // + batch composition: boundary-only, collision-only, mixed batches; boundary, collision, new lanes
-  unsigned long long st[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#define CVR_LAP(k)                                              \
-  {                                                             \
-    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
-    st[k] += now_ - t_lap;                                      \
-    t_lap = now_;                                               \
-  }
-  unsigned long long t_mark = __builtin_amdgcn_s_memtime();
-#endif
 
-#if CVR_STAMPS
-  unsigned long long t_regen = 0;
-#endif
-#if CVR_TAILSTAMPS
-  // start, queues exhausted, end (s_memrealtime, 100 MHz); event batches (total, after
-  // exhaustion); lane-steps after exhaustion (nothing in the track loop: the stamps would
-  // perturb its registers)
-  const unsigned long long ts_start = __builtin_amdgcn_s_memrealtime();
-  unsigned long long ts_ex = 0, ts_n_ev = 0, ts_n_ev_ex = 0, ts_bstart = 0;
-  uint32_t ts_steps_ex = 0;
-#endif
   for (;;) {
     // ================================================= TRACK ==============
-    __builtin_amdgcn_s_setprio(CVR_PRIO_TRACK);
+    __builtin_amdgcn_s_setprio(kPrioTrack);
     // The track state is fresh per outer iteration and parked in the pool
     // before the event code runs, so nothing of it is live across that code
     // (keeps the step loop free of spills).
@@ -578,9 +499,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         break;
       }
       // ---- one Woodcock step (Utilities.cuh:147-152) ---------------------
-#if CVR_STAMPS
-      ++st[3];
-#endif
 #pragma unroll
       for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
         // woodcock_step_core with both draws taken up front: a step that
@@ -607,50 +525,18 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         }
       }
     }
-#if CVR_STAMPS
-    {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      st[1] += now - t_mark;
-      t_mark = now;
-      ++st[2];
-    }
-#endif
     // no path left (new-path slots only count while the queues have paths)
     if (n_lb + n_lc == 0u && n_ready == 0u && (n_ln == 0u || (S.cur[2] & kCurExhausted))) break;
 
     // ================================================= EVENT ==============
-    __builtin_amdgcn_s_setprio(CVR_PRIO_EVENT);
-    // Deferred splats (kDeferSplat): the last batch's escapes, parked in their free slots'
-    // a[] (T, image_id) and filed first on the ln stack, read before this batch's
-    // regeneration can reuse those slots, and issued after this batch's slot loads.
-    float4 dsp = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    bool dlive = false;
-    if constexpr (kDeferSplat) {
-      const uint32_t pd = S.pend;
-      if (lane < (pd >> 8)) {
-        dsp = S.a[S.ln[(pd & 0xFFu) + lane]];
-        dlive = true;
-      }
-    }
-#define CVR_DEFERRED_SPLAT()                 \
-  if (dlive) {                               \
-    PathState q{};                           \
-    q.T = mk3(dsp.x, dsp.y, dsp.z);          \
-    q.image_id = __float_as_uint(dsp.w);     \
-    splat(L, q);                             \
-  }
-    if constexpr (kDeferSplat && CVR_WPOOL_DEFER_SPLAT == 1) { CVR_DEFERRED_SPLAT() }
+    __builtin_amdgcn_s_setprio(kPrioEvent);
     if constexpr (kFlush) {
       const uint32_t pend = S.pend;  // the last batch's ended paths (in-launch output)
-      if (!(CVR_DIAG_COUNT & 4) && pend != 0u) {
+      if (pend != 0u) {
         const uint32_t agg = count_ended(S, L, pend, lane);
         if (lane == 0) S.pend = agg;
       }
     }
-#if CVR_TAILSTAMPS
-    ++ts_n_ev;
-    if (S.cur[2] & kCurExhausted) ts_bstart = __builtin_amdgcn_s_memrealtime();
-#endif
     // Event-code view of the medium: its BSDF / box / albedo fields pass
     // through opaque_s per batch, so values derived from them (HG and box
     // constants) are recomputed in the batch instead of being hoisted to the
@@ -682,7 +568,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 // a further -1.8% on C2 and -1.0% on C3, profiles/round2/ab_kindmin_*.log).
 // New paths fill a
 // boundary batch (a camera path's first event is its GGX entry into the box,
-// the same code) but not a collision batch unless CVR_WPOOL_NEW_FORCE wait:
+// the same code) but not a collision batch unless a whole wave of them waits:
 // beside collisions they would run the whole boundary code on a few lanes
 // (C2 -2.7%, C3 -3%).
 #ifndef CVR_WPOOL_KIND_MIN
@@ -691,43 +577,20 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #ifndef CVR_WPOOL_KIND_MIN_C
 #define CVR_WPOOL_KIND_MIN_C 24
 #endif
-#ifndef CVR_WPOOL_NEW_FORCE
-#define CVR_WPOOL_NEW_FORCE 64
-#endif
       uint32_t tb, tc, tn;
-#ifndef CVR_WPOOL_MAJORITY  // experiment: every batch runs one kind, the one with more items waiting
-#define CVR_WPOOL_MAJORITY 0
-#endif
-      // (once the queues are empty n_ln is the drain rule's stand-in, not new paths)
-      if (CVR_WPOOL_MAJORITY && n_lb + ((S.cur[2] & kCurExhausted) ? 0u : n_ln) >= n_lc) {
+      if (n_lb >= (uint32_t)CVR_WPOOL_KIND_MIN) {
         tb = min(n_lb, 64u);
         tc = 0;
         tn = min(n_ln, 64u - tb);
-      } else if (CVR_WPOOL_MAJORITY) {
+      } else if (n_lc >= (uint32_t)CVR_WPOOL_KIND_MIN_C) {
         tb = 0;
         tc = min(n_lc, 64u);
-        tn = 0;
-      } else if (CVR_WPOOL_KIND_MIN > 0 && n_lb >= (uint32_t)CVR_WPOOL_KIND_MIN) {
-        tb = min(n_lb, 64u);
-        tc = 0;
-        tn = min(n_ln, 64u - tb);
-      } else if (CVR_WPOOL_KIND_MIN_C > 0 && n_lc >= (uint32_t)CVR_WPOOL_KIND_MIN_C) {
-        tb = 0;
-        tc = min(n_lc, 64u);
-        tn = n_ln < (uint32_t)CVR_WPOOL_NEW_FORCE ? 0u : min(n_ln, 64u - tc);
+        tn = n_ln < 64u ? 0u : min(n_ln, 64u - tc);
       } else {
         tb = min(n_lb, 64u);
         tc = min(n_lc, 64u - tb);
         tn = min(n_ln, 64u - tb - tc);
       }
-#if CVR_STAMPS
-      st[10] += (tb > 0u && tc == 0u);
-      st[11] += (tc > 0u && tb == 0u);
-      st[12] += (tb > 0u && tc > 0u);
-      st[13] += tb;
-      st[14] += tc;
-      st[15] += tn;
-#endif
       uint32_t kind = K_NONE, s = 0;
       if (lane < tb) {
         kind = K_BOUNDARY;
@@ -750,9 +613,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       float t_hit = 0.0f;
       bool to_ready = false, to_lb = false, to_ln = false;
       bool truncated = false, escaped = false, seg_first = false, seg_next = false;  // counted by ballots
-#if CVR_STAMPS
-      unsigned long long t_lap = __builtin_amdgcn_s_memtime();
-#endif
       // ---- regeneration (new items): the wave's cursor into the global queues
       const unsigned long long want = __ballot(kind == K_NEW);
       if (want != 0ull) {
@@ -788,10 +648,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             qsel = __shfl(qsel, 0);
             if (b == 0xFFFFFFFFu) {
               cqh |= kCurExhausted;
-#if CVR_TAILSTAMPS
-              ts_ex = __builtin_amdgcn_s_memrealtime();
-              ts_steps_ex = c_steps;
-#endif
               break;
             }
             cqh = qsel | qsel << 8;
@@ -829,8 +685,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             ++nseg;
             seg_first = true;
             if (!aabb_intersect(me, ps.o, ps.d, is)) {
-              if constexpr (kDeferSplat) S.a[s] = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
-              else splat(L, ps);
+              splat(L, ps);
               escaped = true;
               to_ln = true;
               if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
@@ -844,84 +699,19 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           }
         }
       }
-#if CVR_STAMPS
-      CVR_LAP(9)
-#endif
       float4* __restrict__ gT = L.pool_T + (size_t)blockIdx.x * kSlots;  // this wave's event-only slot part
       if (lane < tb + tc) load_full(S, gT, s, ps, is, nseg, t_hit);
       // a filed boundary whose last step passed max_t drew one number too many
       if (lane < tb && !(t_hit <= is.dist)) rng_undo(ps.rng);
-      if constexpr (kDeferSplat && CVR_WPOOL_DEFER_SPLAT == 2) { CVR_DEFERRED_SPLAT() }
-#if CVR_STAMPS
-      CVR_LAP(6)
-#endif
-      // A path's end of event: roulette death, or the AABB test of its next segment
-      // (escape: splat; else its slot is stored).
-#define CVR_FINISH_EVENT(ALIVE)                                                          \
-  if (!(ALIVE)) { /* the path died in roulette */                                     \
-    to_ln = true;                                                                        \
-    if (kFlush) S.meta[s] = ps.image_id; /* the ended path's pixel (in-launch output) */ \
-    if (kRecord) record_end<kSlots>(L, s, ps, 0u, nseg);                               \
-  } else if (L.max_segments && nseg >= L.max_segments) {                                 \
-    truncated = true;                                                                    \
-    to_ln = true;                                                                        \
-    if (kFlush) S.meta[s] = ps.image_id;                                                 \
-    if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);                               \
-  } else {                                                                               \
-    ++nseg;                                                                              \
-    seg_next = true;                                                                     \
-    if (!aabb_intersect(me, ps.o, ps.d, is)) {                                           \
-      splat(L, ps);                                                                      \
-      escaped = true;                                                                    \
-      to_ln = true;                                                                      \
-      if (kFlush) S.meta[s] = ps.image_id;                                               \
-      if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);                             \
-    } else {                                                                             \
-      store_full(S, gT, s, ps, is, nseg);                                                \
-      to_ready = is.inside; /* medium: Woodcock from t = 0 */                            \
-      to_lb = !is.inside;   /* no medium: boundary at isect.dist */                      \
-    }                                                                                    \
-  }
-#ifndef CVR_WPOOL_EARLY_FINISH
-#define CVR_WPOOL_EARLY_FINISH 0
-#endif
-#if CVR_WPOOL_EARLY_FINISH
-      // each kind's paths finish right after their part: the boundary part's stores and
-      // splats are then in flight while the collision part computes
-      if (kind == K_BOUNDARY) {
-        boundary_event(me, ps, is);
-        const bool alive = roulette(ps);
-        CVR_FINISH_EVENT(alive)
-      }
-#if CVR_STAMPS
-      CVR_LAP(7)
-#endif
-      if (kind == K_COLLIDE) {
-        scatter_event<kScatterEps>(me, ps, t_hit);
-        const bool alive = roulette(ps);
-        CVR_FINISH_EVENT(alive)
-      }
-#if CVR_STAMPS
-      CVR_LAP(8)
-#endif
-      const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
-#else
       bool alive = false;
       if (kind == K_BOUNDARY) {
         boundary_event(me, ps, is);
         alive = roulette(ps);
       }
-#if CVR_STAMPS
-      CVR_LAP(7)
-#endif
       if (kind == K_COLLIDE) {
         scatter_event<kScatterEps>(me, ps, t_hit);
         alive = roulette(ps);
       }
-#if CVR_STAMPS
-      CVR_LAP(8)
-#endif
-      if constexpr (kDeferSplat && CVR_WPOOL_DEFER_SPLAT == 3) { CVR_DEFERRED_SPLAT() }
       const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
       if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {  // the path died in roulette
         to_ln = true;
@@ -939,8 +729,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           ++nseg;
           seg_next = true;
           if (!aabb_intersect(me, ps.o, ps.d, is)) {
-            if constexpr (kDeferSplat) S.a[s] = make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id));
-            else splat(L, ps);
+            splat(L, ps);
             escaped = true;
             to_ln = true;
             if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
@@ -952,11 +741,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           }
         }
       }
-#endif
-#undef CVR_FINISH_EVENT
-#if CVR_STAMPS
-      t_regen = __builtin_amdgcn_s_memtime();
-#endif
       // a path's segments are the increments of its nseg (each counted once, as
       // the reference's per-iteration RAYS_STATISTICS count)
       {
@@ -972,15 +756,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       const unsigned long long mr = __ballot(to_ready), mb = __ballot(to_lb), mn = __ballot(to_ln);
       if (to_ready) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)s;
       if (to_lb) S.lb[n_lb + lane_rank(mb)] = (uint8_t)s;
-      if constexpr (kDeferSplat) {
-        // escapes first on the ln stack: the next batch splats ln[n_ln, + their count)
-        const unsigned long long mx = __ballot(escaped);
-        const uint32_t n_x = (uint32_t)__popcll(mx);
-        if (to_ln) S.ln[n_ln + (escaped ? lane_rank(mx) : n_x + lane_rank(mn & ~mx))] = (uint8_t)s;
-        if (lane == 0) S.pend = n_x != 0u ? n_ln | n_x << 8 : 0u;
-      } else if (to_ln) {
-        S.ln[n_ln + lane_rank(mn)] = (uint8_t)s;
-      }
+      if (to_ln) S.ln[n_ln + lane_rank(mn)] = (uint8_t)s;
       if constexpr (kFlush) {
         // in-launch output: the ended paths (their slots' meta holds the pixel) are counted
         // at the next batch
@@ -1011,41 +787,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         n_ln = d ? 64u - min(64u, (n_live * d + d) / (d + 1u)) : 0u;
       }
     }
-#if CVR_STAMPS
-    {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      st[0] += now - t_mark;
-      st[5] += t_regen - t_mark;
-      t_mark = now;
-    }
-#endif
-#if CVR_TAILSTAMPS
-    // drain timeline: per batch after exhaustion, (start - exhaustion) | batch duration << 32 |
-    // paths filed as boundary events << 48 | collisions << 56 (10 ns units)
-    if (ts_bstart) {
-      if (ts_n_ev_ex < 48u && lane == 0u) {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        (L.stats + kStampWord + (size_t)gridDim.x * 10)[(size_t)blockIdx.x * 48 + ts_n_ev_ex] =
-            ((ts_bstart - ts_ex) & 0xFFFFFFFFull) | (min(now - ts_bstart, 0xFFFFull) << 32) |
-            ((unsigned long long)min(n_lb, 255u) << 48) | ((unsigned long long)min(n_ready, 255u) << 56);
-      }
-      ++ts_n_ev_ex;
-      ts_bstart = 0;
-    }
-#endif
   }
 
-  if constexpr (kDeferSplat) {  // the last batch's escapes
-    const uint32_t pd = S.pend;
-    if (lane < (pd >> 8)) {
-      const float4 f = S.a[S.ln[(pd & 0xFFu) + lane]];
-      PathState q{};
-      q.T = mk3(f.x, f.y, f.z);
-      q.image_id = __float_as_uint(f.w);
-      splat(L, q);
-    }
-  }
-#undef CVR_DEFERRED_SPLAT
   if constexpr (kFlush) {
     const uint32_t pend = S.pend;  // raw: the last batch's ended paths
     if (pend != 0u) {
@@ -1067,25 +810,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     if (lane < (uint32_t)STAT_COUNT && w[lane])
       __hip_atomic_fetch_add(gmem(L.stats + lane), w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-#if CVR_TAILSTAMPS
-  {
-    unsigned long long sx = c_steps - ts_steps_ex;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sx += __shfl_xor(sx, off);
-    const unsigned long long ts_end = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long hw = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
-    const unsigned long long v[10] = {ts_start, 0ull, ts_ex, ts_end, 0ull, ts_n_ev, 0ull, ts_n_ev_ex, sx, hw};
-    if (lane < 10u) L.stats[kStampWord + (size_t)blockIdx.x * 10 + lane] = v[lane];
-  }
-#endif
-#if CVR_STAMPS
-  {
-    const unsigned long long now = __builtin_amdgcn_s_memtime();
-    st[1] += now - t_mark;
-  }
-  if (lane == 0)
-    for (int k = 0; k < 16; ++k) atomicAdd(L.stats + 16 + k, st[k]);
-#endif
 }
 
 // Instances: 5 waves per SIMD (the default budget) for every medium layout, with and
@@ -1135,12 +859,11 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
 }
 
 uint32_t wpool_slots(int waves, bool sparse) {
-  constexpr bool ss = CVR_WPOOL_SPLIT_SPARSE;
-  if (sparse) return waves == 5 ? PoolSize<5, ss>::value : PoolSize<4, ss>::value;
-  return waves == 5   ? PoolSize<5, true>::value
-         : waves == 6 ? PoolSize<6, true>::value
-         : waves == 3 ? PoolSize<3, true>::value
-                      : PoolSize<4, true>::value;
+  if (sparse) return waves == 5 ? PoolSize<5>::value : PoolSize<4>::value;
+  return waves == 5   ? PoolSize<5>::value
+         : waves == 6 ? PoolSize<6>::value
+         : waves == 3 ? PoolSize<3>::value
+                      : PoolSize<4>::value;
 }
 
 hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu) {

@@ -1,13 +1,14 @@
-"""Multi-GPU driver: one process per GPU, sample (path-id) sharding, one
-RCCL all-reduce of the framebuffer.
+"""Multi-GPU driver: one process per GPU; by default pixel-block shards with
+no collective in the data path.
 
 Why this decomposition: paths are independent and the only
 shared output is the additive fp32 framebuffer.  With the RNG bound to the
-path id, a path renders the same on any rank, so splitting the path-id range
-[0, n_paths) into contiguous shards changes nothing but the order of the fp32
-sums.  The only exchange is one sum-reduce of W*H*4 floats over xGMI (16 MiB
-at 1024^2) per render.  Image tiles are not used for the split because tile
-costs are very uneven (background vs volume).
+path id, a path renders the same on any rank, so any partition of the
+path-id set changes nothing but the order of the fp32 sums.  The default
+(block shards, below) partitions it by 8x8 pixel blocks, so the ranks' pixels
+are disjoint and there is nothing to sum: RCCL carries only barriers and the
+max-over-ranks time.  The other modes, which share pixels between ranks, sum
+the framebuffers with one RCCL reduce-scatter per render.
 
 Weak scaling (bench.py): each rank renders its own `iterations` samples per
 pixel; the job renders iterations*world samples per pixel in total.
@@ -184,16 +185,19 @@ class HostImage:
         self._mm = mm
         self.flat = torch.from_numpy(mm)
         self.pinned = False
-        try:  # hipHostRegister the mapping (plumbing; the copy is correct either way)
-            if not pin:
-                raise OSError("not pinned")
-            hip = ctypes.CDLL("libamdhip64.so")
-            hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
-            self._hip = hip
-            if hip.hipHostRegister(ctypes.c_void_p(self.flat.data_ptr()), nbytes, 2) == 0:  # hipHostRegisterMapped
-                self.pinned = self._registered = True
-        except OSError:
-            pass
+        if not pin:  # host tensors only (the gloo CPU tests)
+            return
+        # hipHostRegister the mapping: the ranks' kernels store their blocks into it over PCIe.
+        # An unpinned image would turn every render's output step into a synchronous host-side
+        # gather inside the timed region, so a failure here ends the run instead.
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+        self._hip = hip
+        rc = hip.hipHostRegister(ctypes.c_void_p(self.flat.data_ptr()), nbytes, 2)  # hipHostRegisterMapped
+        if rc != 0:
+            raise RuntimeError(f"rank {rank}: hipHostRegister of the shared host image {self.path} failed "
+                               f"(hipError {rc}); refusing to run with an unpinned image")
+        self.pinned = self._registered = True
 
     def slice(self, r):
         return self.flat[r * self.chunk:(r + 1) * self.chunk]
@@ -233,7 +237,9 @@ def blocks_to_host(acc_flat, host: "HostImage", width: int, height: int, scale: 
     GPU one kernel on the current stream stores into the pinned / registered
     image (cvr_blocks_to_host); host tensors (the gloo CPU tests) are indexed."""
     n = width * height * 4
-    if acc_flat.is_cuda and host.pinned:
+    if acc_flat.is_cuda:
+        if not host.pinned:
+            raise RuntimeError("blocks_to_host: a device framebuffer needs a pinned host image")
         import torch
         from . import _lib
         _lib.blocks_to_host(acc_flat.data_ptr(), host.flat.data_ptr(), width, height, host.rank, host.world,
@@ -242,10 +248,7 @@ def blocks_to_host(acc_flat, host: "HostImage", width: int, height: int, scale: 
     import torch
     idx = torch.from_numpy(block_pixel_index(width, height, host.rank, host.world))
     src = acc_flat[:n].view(-1, 4)
-    if src.is_cuda:
-        src = src[idx.to(src.device)].cpu()
-    else:
-        src = src[idx]
+    src = src[idx]
     host.flat[:n].view(-1, 4)[idx] = src / scale
 
 

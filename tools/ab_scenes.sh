@@ -1,4 +1,4 @@
-# A/B of experiment builds vs HEAD: bash tools/job_ab2.sh ROUNDS "VARIANTS" LIB...
+# A/B of experiment builds vs HEAD: bash tools/ab_scenes.sh ROUNDS "VARIANTS" LIB...
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

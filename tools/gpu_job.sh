@@ -37,7 +37,6 @@ for step in "$@"; do
     tune) run tune 600 python3 tools/tune.py ;;
     stamps) run stamps 300 python3 tools/stamps.py ;;
     poolstamps) run poolstamps 300 python3 tools/poolstamps.py ;;
-    wpoolstamps) run wpoolstamps 300 python3 tools/wpoolstamps.py ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc_sq" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 1 --variants "regenerationSK:ev=16,chunk=128" ;;
     pmc_a) run pmc_a 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc_a" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     pmc_b) run pmc_b 600 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc_b" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
