@@ -115,6 +115,7 @@ def load() -> C.CDLL:
         "cvr_scene_is_sparse": (I32, [P]),
         "cvr_set_camera": (I32, [P, FP, FP, FP]),
         "cvr_set_resolution": (I32, [P, U32, U32]),
+        "cvr_get_resolution": (I32, [P, C.POINTER(U32), C.POINTER(U32)]),
         "cvr_set_offset": (I32, [P, U32, U32]),
         "cvr_set_iterations": (I32, [P, U32]),
         "cvr_set_path_range": (I32, [P, U64, U64]),
@@ -392,7 +393,14 @@ class Context:
 
     def set_resolution(self, w, h):
         self._c(load().cvr_set_resolution(self._h, w, h))
-        self.resolution = (w, h)
+
+    @property
+    def resolution(self):
+        """The tile resolution the library renders now (cvr_get_resolution): render_image /
+        render_tiles set it to their tile size too."""
+        w, h = C.c_uint32(), C.c_uint32()
+        self._c(load().cvr_get_resolution(self._h, C.byref(w), C.byref(h)))
+        return w.value, h.value
 
     def set_offset(self, x, y):
         self._c(load().cvr_set_offset(self._h, x, y))
@@ -508,7 +516,9 @@ class Context:
         st = Stats() if stats else None
         img = None
         if host_ptr is None:
-            w, h = self.resolution
+            w, h = self.resolution  # the library's own tile size (what cvr_render_frame writes)
+            if w == 0 or h == 0:
+                raise CvrError(-3, "render_frame: no resolution set")
             img = np.zeros((h, w, 4), np.float32)
             host_ptr = img.ctypes.data
         self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), parts, C.byref(st) if stats else None))

@@ -997,6 +997,13 @@ int cvr_set_resolution(cvr_ctx* c, uint32_t w, uint32_t h) {
   return ensure_output(c);
 }
 
+int cvr_get_resolution(const cvr_ctx* c, uint32_t* w, uint32_t* h) {
+  if (!c || !w || !h) return set_err(nullptr, CVR_ERR_INVALID, "NULL argument");
+  *w = c->tile_w;
+  *h = c->tile_h;
+  return CVR_OK;
+}
+
 int cvr_set_offset(cvr_ctx* c, uint32_t x, uint32_t y) {
   if (!c) return set_err(nullptr, CVR_ERR_INVALID, "NULL ctx");
   c->off[0] = x;
@@ -1798,8 +1805,10 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* s
     int lo = 0, hi = 0;
     HIP_TRY(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_TRY(c, hipStreamCreateWithPriority(&c->frame_copy, hipStreamNonBlocking, hi));
-    for (auto& e : c->frame_ev) HIP_TRY(c, hipEventCreate(&e));
   }
+  // the same events as render_frame_flush's (created once, whichever path comes first)
+  if (!c->frame_ev[0])
+    for (auto& e : c->frame_ev) HIP_TRY(c, hipEventCreate(&e));
   if (c->frame_px < px) {
     HIP_TRY(c, hipStreamSynchronize(c->frame_copy));
     if (c->d_frame) (void)hipFree(c->d_frame);

@@ -96,7 +96,8 @@ typedef enum {
                                  here).  Scheduling only: results are unchanged. */
   CVR_OPT_WORLD_TO_AABB = 18,  /* quirk Q4: 0 (default) the reference's worldToAABB, p - min/extent
                                  (operator precedence, Utilities.cuh:129-132); 1 the intended
-                                 (p - min)/extent, computed as fma(p, 1/extent, -min/extent).  The two
+                                 (p - min)/extent, computed as (p - box_min) * ((res - 1)/extent) (the
+                                 grid scale folded in: shift = box_min, gx = (res - 1)/extent).  The two
                                  agree for the unit box of VDB/Raw/MHD scenes. */
   CVR_OPT_SUBQUEUES = 20,      /* wave-pool scheduler: work queues per XCD band (1..8, default 8), each
                                  over a contiguous part of the band, so that small dequeue chunks do not
@@ -218,6 +219,10 @@ int cvr_set_camera(cvr_ctx* ctx, const float inv_view[12], const float raster_to
                    const float full_res[2]);
 /* setResolution(tile_dim) */
 int cvr_set_resolution(cvr_ctx* ctx, uint32_t tile_w, uint32_t tile_h);
+/* The tile resolution the context renders now (set by cvr_set_resolution, or
+ * by cvr_render_image / cvr_render_tiles to their tile size): the size of the
+ * host image cvr_render_frame writes (tile_w * tile_h float4).  Extension. */
+int cvr_get_resolution(const cvr_ctx* ctx, uint32_t* tile_w, uint32_t* tile_h);
 /* copyOffset(tile origin) */
 int cvr_set_offset(cvr_ctx* ctx, uint32_t x, uint32_t y);
 /* setNIterations: n_paths = tile_w * tile_h * iterations */
@@ -347,7 +352,10 @@ typedef struct cvr_render_desc {
 /* Render all tiles: per tile set offset, launch, normalise by iterations
  * into the image, reset.  `device_image` (W*H float4, may be NULL) receives
  * the normalised image on the device, `host_image` (may be NULL) a copy.
- * Pixels outside tile_dim*n_tiles are not written (Q1). */
+ * Pixels outside tile_dim*n_tiles are not written (Q1).  stats->kernel_ms is
+ * the sum of the tile launches' HIP-event times; one tile into host memory
+ * only (no device_image) runs as cvr_render_frame, whose kernel_ms spans the
+ * clear, the launch and its in-launch output. */
 int cvr_render_image(cvr_ctx* ctx, const cvr_render_desc* desc, void* device_image, float* host_image,
                      cvr_stats* stats);
 /* Tile-sharded variant (tile k -> GPU k): render only the

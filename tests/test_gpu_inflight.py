@@ -272,6 +272,23 @@ def c_out(c):
     return c.copy_output(W, H), c.stats()
 
 
+def _launch_copy(c, w, h):
+    """The launcher-level render (clear, cvr_launch_render, cvr_copy_output / ITERS),
+    with the seed render_image's tile 0 has: a path independent of cvr_render_frame
+    (render_image of one tile into host memory goes through cvr_render_frame)."""
+    c.set_resolution(w, h)
+    c.set_iterations(ITERS)
+    c.set_offset(0, 0)
+    c.set_seed(0)
+    c.clear_output()
+    c.launch_render()
+    c.synchronize()
+    img = c.copy_output(w, h, float(ITERS))
+    st = c.stats()
+    c.set_seed(0)
+    return img, st
+
+
 @pytest.mark.parametrize("kernel,parts,res", [("regenerationSK", 3, (256, 256)), ("regenerationSK", 2, (256, 200)),
                                               ("sortingSK", 3, (256, 256)), ("regenerationSK", 1, (256, 256)),
                                               ("regenerationSK", 3, (250, 256)), ("naiveSK", 3, (256, 256)),
@@ -279,11 +296,13 @@ def c_out(c):
 def test_render_frame_equals_render_image(cvr, kernel, parts, res):
     """cvr_render_frame (one synchronous render, the launch split into bands
     of block rows on helper contexts, each band's normalise + copy overlapping
-    the later bands) leaves the same image in host memory as render_image's
-    single launch, with the same counters; kernels and sizes that cannot take
-    bands (naiveSK, a side that is not a multiple of 8) render as one part.
-    Repeated calls reuse the helpers; a second medium loaded into the owner is
-    what the helpers render next."""
+    the later bands; one part: the in-launch output) leaves the same image in
+    host memory as a plain launch + copy, with the same counters; kernels and
+    sizes that cannot take bands (naiveSK, a side that is not a multiple of 8)
+    render as one part.  Repeated calls reuse the helpers; a second medium
+    loaded into the owner is what the helpers render next.  render_frame(None)
+    sizes its array from the library's resolution, which render_image sets to
+    its tile size."""
     w, h = res
     scene = cvr.Scene.synthetic("manix")
     c = cvr.Context(0, kernel)
@@ -291,9 +310,11 @@ def test_render_frame_equals_render_image(cvr, kernel, parts, res):
     iv, r2v = cvr.default_camera(w, h)
     c.set_camera(iv, r2v, (w, h))
     c.init()
-    ref, rst = c.render_image(w, h, (1, 1), ITERS)
-    c.set_resolution(w, h)
+    c.set_resolution(16, 8)
     c.set_iterations(ITERS)
+    small, _ = c.render_image(w, h, (1, 1), ITERS)  # leaves the context at the w x h tile
+    assert c.resolution == (w, h) and small.shape == (h, w, 4)
+    ref, rst = _launch_copy(c, w, h)
     for rep in range(2):
         c.set_seed(0)  # render_image's tile 0 seed; both calls advance it as reset() does
         img, st = c.render_frame(None, parts)
@@ -305,11 +326,7 @@ def test_render_frame_equals_render_image(cvr, kernel, parts, res):
     # another medium in the owner: the helpers follow it
     other = cvr.Scene.synthetic("hetvol")
     c.set_medium(other.medium)
-    c.set_seed(0)
-    ref2, rst2 = c.render_image(w, h, (1, 1), ITERS)
-    c.set_resolution(w, h)
-    c.set_iterations(ITERS)
-    c.set_seed(0)
+    ref2, rst2 = _launch_copy(c, w, h)
     img2, st2 = c.render_frame(None, parts)
     assert st2.steps == rst2.steps and st2.escaped == rst2.escaped
     assert_pixels_close(img2[..., :3], ref2[..., :3], ITERS, "render_frame after a new medium")

@@ -23,7 +23,7 @@ for step in "$@"; do
   case $step in
     info) run info 60 bash -c 'nproc; grep -m1 "model name" /proc/cpuinfo; grep -o -m1 -w fma /proc/cpuinfo; rocm-smi --showproductname 2>/dev/null | head -20; python3 -c "import torch;print(torch.__version__, torch.cuda.device_count())"' ;;
     smoke) run smoke 400 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
-    pytest) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q -x --timeout 900 -p no:cacheprovider ;;
+    pytest) run pytest_gpu 1100 python3 -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     pytestall) run pytest_gpu 1100 python3 -m pytest tests -m gpu -q --timeout 900 -p no:cacheprovider ;;
     bench) run bench 600 python3 bench.py --steps 10 --warmup 2 ;;
     benchd) run benchd 600 python3 bench.py --steps 20 --warmup 5 ;;
@@ -49,6 +49,10 @@ for step in "$@"; do
     prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline ;;
     pmcf:*) sc=${step#pmcf:}; mkdir -p "$OUT/pmcf_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcf_$sc/libcvr.sha256"; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
     pmcw:*) sc=${step#pmcw:}; mkdir -p "$OUT/pmcw_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcw_$sc/libcvr.sha256"; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    # VALU issue (tools/valu.py): pmcv:SCENE
+    pmcv:*) sc=${step#pmcv:}; mkdir -p "$OUT/pmcv_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcv_$sc/libcvr.sha256"; run pmcv_$sc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
+    # the driver's default bench line
+    benchdef) run benchdef 600 python3 bench.py ;;
     # arbitrary counters on a scene's bench run: pmcx:SCENE:CTR1,CTR2,...
     pmcx:*) IFS=: read -r _ sc ctrs <<< "$step"; d=pmcx_${sc}_${ctrs//,/_}; mkdir -p "$OUT/$d"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/$d/libcvr.sha256"; run $d 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$OUT/$d" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
     # A/B of experiment builds: ab:SCENE:ROUNDS:variant1,variant2,...
