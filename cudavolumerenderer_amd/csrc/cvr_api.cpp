@@ -81,7 +81,6 @@ struct cvr_ctx {
   float* d_leaf_density = nullptr;
   float4* d_leaf_albedo = nullptr;
   uint32_t* d_sbounds = nullptr;
-  uint32_t* d_scoarse = nullptr;
   uint32_t* d_block_perm = nullptr;  // cvr_set_block_order
   void* d_rec_active = nullptr;      // cvr_trace_launch: records of the launch in progress
   uint32_t block_perm_n = 0;
@@ -677,8 +676,6 @@ static void free_sparse(cvr_ctx* c) {
   if (c->d_leaf_density) (void)hipFree(c->d_leaf_density);
   if (c->d_leaf_albedo) (void)hipFree(c->d_leaf_albedo);
   if (c->d_sbounds) (void)hipFree(c->d_sbounds);
-  if (c->d_scoarse) (void)hipFree(c->d_scoarse);
-  c->d_scoarse = nullptr;
   c->d_leaves = nullptr;
   c->d_leaf_density = nullptr;
   c->d_leaf_albedo = nullptr;
@@ -712,7 +709,6 @@ static void fill_medium_common(cvr::MediumParams& m, const uint32_t res[3], cons
   m.ay = roughness[1];
   m.eta = eta;
   m.inv_eta = 1.0f / eta;
-  m.bq = (float)((1.0 / 254.0) * (1.0 + 1.0 / 65536.0));
 }
 
 int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
@@ -750,13 +746,14 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   if (c->d_bounds) (void)hipFree(c->d_bounds);
   c->d_bounds = nullptr;
   const float sigma = md->scale * md->max_density;
-  uint32_t bnx = 0, bny = 0;
+  uint32_t bnx = 0, bny = 0, bsentinel = 0;
   if (c->bound_shift && sigma > 0.0f && std::isfinite(sigma) && md->scale > 0.0f) {
     const uint32_t B = 1u << c->bound_shift;
     bnx = (md->res[0] + B - 1) / B;
     bny = (md->res[1] + B - 1) / B;
     const size_t nb = (size_t)bnx * bny * ((md->res[2] + B - 1) / B);
-    HIP_TRY(c, hipMalloc(&c->d_bounds, nb));
+    bsentinel = (uint32_t)nb;  // the no-bound entry past the last brick (k_build_bounds writes it)
+    HIP_TRY(c, hipMalloc(&c->d_bounds, nb + 1));
     HIP_TRY(c, cvr::launch_build_bounds(c->d_density, md->res[0], md->res[1], md->res[2], c->bound_shift,
                                         md->max_density, c->d_bounds, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -768,6 +765,7 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
   m.bnx = bnx;
   m.bny = bny;
   m.bnxy = bnx * bny;
+  m.bsentinel = bsentinel;
   m.cells = c->d_cells;
   m.density = c->d_density;
   m.albedo = c->d_albedo;
@@ -783,55 +781,6 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
     }
   }
   c->have_medium = true;
-  return CVR_OK;
-}
-
-// Two-level sparse bounds (cvr_walk.h MediumParams::scoarse): from the full
-// brick-word grid m.sbounds, one word per macro of 4^3 bricks (the largest q
-// of its bricks, and the index of its compact block of 64 brick words), and
-// the blocks of the macros whose bricks are not all empty.  C5: the full grid
-// is 16.8 MB, larger than an XCD's 4 MB L2, so most Woodcock steps missed L2
-// on their brick word; the macro words take 0.5 MB, and the steps in empty
-// macros (most of the volume) read nothing else.
-static int build_two_level_bounds(cvr_ctx* c, cvr::MediumParams& m, uint32_t bnz) {
-  const uint32_t bnx = m.bnx, bny = m.bny;
-  const size_t nb = (size_t)bnx * bny * bnz;
-  std::vector<uint32_t> full(nb);
-  HIP_TRY(c, hipMemcpy(full.data(), c->d_sbounds, nb * sizeof(uint32_t), hipMemcpyDeviceToHost));
-  const uint32_t cnx = (bnx + 3) / 4, cny = (bny + 3) / 4, cnz = (bnz + 3) / 4;
-  const size_t nm = (size_t)cnx * cny * cnz;
-  std::vector<uint32_t> coarse(nm, 0u), blocks;
-  for (uint32_t mz = 0; mz < cnz; ++mz)
-    for (uint32_t my = 0; my < cny; ++my)
-      for (uint32_t mx = 0; mx < cnx; ++mx) {
-        uint32_t q = 0;
-        uint32_t blk[64] = {0};
-        for (uint32_t k = 0; k < 64; ++k) {
-          const uint32_t bx = mx * 4 + (k & 3), by = my * 4 + ((k >> 2) & 3), bz = mz * 4 + (k >> 4);
-          if (bx >= bnx || by >= bny || bz >= bnz) continue;
-          blk[k] = full[((size_t)bz * bny + by) * bnx + bx];
-          q = std::max(q, blk[k] >> 24);
-        }
-        uint32_t idx = 0;
-        if (q > 0) {
-          idx = (uint32_t)(blocks.size() / 64);
-          if (idx >= (1u << 24)) return set_err(&c->err, CVR_ERR_UNSUPPORTED, "too many non-empty macro bricks");
-          blocks.insert(blocks.end(), blk, blk + 64);
-        }
-        coarse[((size_t)mz * cny + my) * cnx + mx] = (q << 24) | idx;
-      }
-  if (blocks.empty()) blocks.assign(64, 0u);
-  (void)hipFree(c->d_sbounds);
-  c->d_sbounds = nullptr;
-  m.sbounds = nullptr;
-  HIP_TRY(c, hipMalloc(&c->d_sbounds, blocks.size() * sizeof(uint32_t)));
-  HIP_TRY(c, hipMemcpy(c->d_sbounds, blocks.data(), blocks.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-  HIP_TRY(c, hipMalloc(&c->d_scoarse, nm * sizeof(uint32_t)));
-  HIP_TRY(c, hipMemcpy(c->d_scoarse, coarse.data(), nm * sizeof(uint32_t), hipMemcpyHostToDevice));
-  m.sbounds = c->d_sbounds;
-  m.scoarse = c->d_scoarse;
-  m.cnx = cnx;
-  m.cnxy = cnx * cny;
   return CVR_OK;
 }
 
@@ -918,9 +867,10 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
   const uint32_t bnz = (res[2] + B - 1) / B;
   const size_t nb = (size_t)m.bnx * m.bny * bnz;
   m.bnxy = m.bnx * m.bny;
-  if ((uint64_t)m.bnx * m.bny >= (1ull << 24) || nb > 0xFFFFFFFFull)
+  if ((uint64_t)m.bnx * m.bny >= (1ull << 24) || nb >= 0xFFFFFFFFull)
     return set_err(&c->err, CVR_ERR_UNSUPPORTED, "sparse grid has too many bricks (%zu)", nb);
-  HIP_TRY(c, hipMalloc(&c->d_sbounds, nb * sizeof(uint32_t)));
+  m.bsentinel = (uint32_t)nb;  // the no-bound word past the last brick (k_build_sparse_bounds writes it)
+  HIP_TRY(c, hipMalloc(&c->d_sbounds, (nb + 1) * sizeof(uint32_t)));
   if (c->use_cells) HIP_TRY(c, hipMalloc(&c->d_cells, ncl * 1024 * sizeof(float4)));
   uint32_t *d_coords = nullptr, *d_slot = nullptr;
   hipError_t e = hipMalloc(&d_coords, coords.size() * sizeof(uint32_t));
@@ -936,10 +886,6 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
   if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "sparse medium build: %s", hipGetErrorString(e));
   m.cells = c->d_cells;
   m.sbounds = c->d_sbounds;
-#if CVR_SPARSE_2LEVEL
-  r = build_two_level_bounds(c, m, bnz);
-  if (r) return r;
-#endif
   c->n_cell_leaves = ncl;
   c->have_medium = true;
   return CVR_OK;

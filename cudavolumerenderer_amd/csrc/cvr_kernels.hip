@@ -424,6 +424,22 @@ __global__ __launch_bounds__(256) void k_build_cells(const float* __restrict__ D
 // MediumParams::bounds.  One work-item per brick: the max over the voxels
 // its cells interpolate (cells [b*B, b*B+B-1] use voxels up to b*B+B, clamped
 // as texel() clamps), quantised upwards to q/254 of max_density.
+// Brick-bound code (MediumParams::bounds, bound_value) of a brick whose
+// largest density is mx: the smallest c with bound_value(c) >= (mx /
+// max_density) (1 + 2^-16).  The test value fl(fl(scale rho) inv_sigma) of a
+// point whose 8 corners are <= mx is <= mx / max_density (1 + 14 u), u = 2^-24
+// (three fma lerps of values <= mx, then two rounded products), so the code
+// bounds every test value of the brick.  255 (no bound): NaN / inf densities,
+// or mx above the majorant (Q15: XML densities may exceed it).
+__device__ uint32_t bound_code(float mx, float max_density, bool nan) {
+  const double r = (double)mx / (double)max_density;
+  if (nan || !(r <= 1.0)) return 255u;
+  const double target = r * (1.0 + 1.0 / 65536.0);
+  uint32_t c = 0;
+  while (c < 255u && (double)bound_value(c) < target) ++c;
+  return c;
+}
+
 __global__ __launch_bounds__(256) void k_build_bounds(const float* __restrict__ D, uint32_t rx, uint32_t ry,
                                                       uint32_t rz, uint32_t bshift, uint32_t bnx, uint32_t bny,
                                                       uint32_t bnz, float max_density, uint8_t* __restrict__ q) {
@@ -442,13 +458,9 @@ __global__ __launch_bounds__(256) void k_build_bounds(const float* __restrict__ 
           nan |= !(v == v) || v == __builtin_inff();
           mx = fmaxf(mx, v);
         }
-    const double r = (double)mx / (double)max_density;
-    uint32_t v;
-    if (nan || !(r <= 1.0)) v = 255u;  // no bound (Q15: XML densities may exceed the majorant)
-    else if (mx == 0.0f) v = 0u;
-    else v = min(254u, (uint32_t)ceil(r * 254.0 * (1.0 + 1e-6)));
-    q[i] = (uint8_t)v;
+    q[i] = (uint8_t)bound_code(mx, max_density, nan);
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) q[nb] = 255u;  // MediumParams::bsentinel: no bound
 }
 
 // ------------------------------------------------------ sparse medium -----
@@ -504,13 +516,11 @@ __global__ __launch_bounds__(256) void k_build_sparse_bounds(MediumParams m, con
             nan |= !(d == d) || d == __builtin_inff();
             mx = fmaxf(mx, d);
           }
-      const double r = (double)mx / (double)max_density;
-      if (nan || !(r <= 1.0)) v = 255u;
-      else if (mx == 0.0f) v = 0u;
-      else v = min(254u, (uint32_t)ceil(r * 254.0 * (1.0 + 1e-6)));
+      v = bound_code(mx, max_density, nan);
     }
     sb[i] = (v << 24) | slot;
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) sb[nb] = 255u << 24;  // MediumParams::bsentinel: no bound, slot 0
 }
 
 // ---------------------------------------------------------- launchers -----

@@ -122,31 +122,26 @@ struct MediumParams {
   const float4* __restrict__ cells;   // 2 * rx*ry*rz float4, may be null
   const float4* __restrict__ albedo;  // rx*ry*rz float4 (rgb, w=1)
   // Brick bounds (DESIGN.md §Brick bounds): for each brick of 2^bshift cells
-  // per axis, q = a u8 upper bound of every density the brick's cells can
-  // interpolate, in units of max_density/254 (255 = no bound).  A Woodcock
-  // tentative point whose brick threshold q*bq is below its test draw is a
-  // null collision whatever the exact density is, so the cell is not fetched.
-  // May be null (every point is fetched).
+  // per axis, a u8 code c of an upper bound of every Woodcock test value
+  // fl(fl(scale*rho)*inv_sigma) the brick's cells can give, as a minifloat
+  // (bound_value: 4 exponent, 4 mantissa bits; 255 = 1.9375 = no bound, as
+  // every test draw is <= 1).  A Woodcock tentative point whose brick bound is
+  // below its test draw is a null collision whatever the exact density is, so
+  // the cell is not fetched.  Entry bsentinel (one past the last brick) holds
+  // 255: points off the cell grid read it.  May be null (every point is fetched).
   const uint8_t* __restrict__ bounds;
   uint32_t bshift, bnx, bny;  // brick size log2, bricks per x / y row
   uint32_t bnxy;              // bnx * bny (< 2^24)
-  float bq;                   // (1/254)(1 + 2^-16): q -> bound on rho*inv_sigma
+  uint32_t bsentinel;         // index of the no-bound entry of bounds / sbounds
   // Sparse storage (cvr_set_medium_sparse; all null for a dense medium):
   // 8^3-voxel leaves, slot = leaves[leaf index] or CVR_NO_LEAF (density 0,
   // albedo albedo_bg).  `density`/`albedo` are then null, `cells` is the
   // cell-leaf pool (512 cells of 2 float4 per slot, slot 0 all zero) and
-  // `sbounds` replaces `bounds`: per brick, q << 24 | cell-leaf slot.
+  // `sbounds` replaces `bounds`: per brick, c << 24 | cell-leaf slot.
   const uint32_t* __restrict__ leaves;
   const float* __restrict__ leaf_density;  // slot * 512 + local
   const float4* __restrict__ leaf_albedo;  // may be null: albedo_bg everywhere
   const uint32_t* __restrict__ sbounds;
-  // Two-level sparse bounds (CVR_SPARSE_2LEVEL): one word per macro of 4^3
-  // bricks, q_macro << 24 | block, q_macro the largest q of its bricks; the
-  // brick words of macros with q_macro > 0 are stored as compact blocks of 64
-  // (brick (x,y,z) & 3 at x | y << 2 | z << 4) in `sbounds`.  Null: `sbounds`
-  // is the full brick-word grid (bnx, bnxy).
-  const uint32_t* __restrict__ scoarse;
-  uint32_t cnx, cnxy;                      // macros per x row / per xy plane
   uint32_t lnx, lny;                       // leaves per x / y row
   V3 albedo_bg;
   uint32_t rx, ry, rz;
@@ -175,13 +170,12 @@ struct MediumParams {
   uint32_t albedo_uniform;
 };
 
-// 1: sparse media bound their Woodcock points with macro words first (see
-// MediumParams::scoarse).  Off by default: on C5 it halves the L2 misses and
-// the memory-side traffic (386 -> 208 GB per launch) but the second dependent
-// load makes the kernel 4.6% slower.
-#ifndef CVR_SPARSE_2LEVEL
-#define CVR_SPARSE_2LEVEL 0
-#endif
+// Brick-bound code -> bound (MediumParams::bounds): the float with bits
+// (c << 19) + (112 << 23), one v_lshl_add_u32.  c = 16 e + m stands for
+// 2^(e - 15) (1 + m / 16): 0 is 2^-15 (below every test draw but 2^-15 of
+// them), 255 is 1.9375 (above every test draw: no bound).
+constexpr uint32_t kBoundBias = 112u << 23;
+CVR_DEV float bound_value(uint32_t c) { return __uint_as_float((c << 19) + kBoundBias); }
 
 // u32 division by a launch-invariant divisor: q = (t + ((u - t) >> s1)) >> s2
 // with t = mulhi(u, m) (round-up method, exact for every u32 and d >= 1;
@@ -464,11 +458,13 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 // draws it right after the lookup and nothing in between consumes the RNG,
 // so the stream is the same.  Brick bounds (MediumParams::bounds): the exact
 // test is !(fl(fl(scale*rho)*inv_sigma) < xi) with rho the trilinear density
-// of the cell, and rho <= bound*(1 + 9u) (three fma lerps of values <=
-// bound), so fl(fl(scale*rho)*inv_sigma) <= rho/max_density*(1 + 14u) <=
-// q*bq: when q*bq < xi the point is a null collision whatever rho is, and the
-// cell is not fetched.  Points whose lower corner lies outside the grid
-// (quirk Q5 taps, NaN) use q = 255 (never bounded out) and the 8-tap gather.
+// of the cell, and rho <= mx*(1 + 9u) for mx the brick's largest density
+// (three fma lerps of values <= mx), so fl(fl(scale*rho)*inv_sigma) <=
+// mx/max_density*(1 + 14u) <= bound_value(c) (k_build_bounds' bound_code):
+// when that bound is below xi the point is a null collision whatever rho is,
+// and the cell is not fetched.  Points whose lower corner lies outside the
+// grid (quirk Q5 taps, NaN) read the sentinel entry (no bound) and the 8-tap
+// gather.
 //
 // Result: 0 null collision (continue), 1 t > max_t (no density evaluation),
 // 2 real collision with t < max_t, 3 real collision at t == max_t (the
@@ -480,9 +476,8 @@ struct WoodcockPoint {
   float cx, cy, cz;     // grid coordinate (DeviceVolume::volumeToGrid)
   float fx1, fy1, fz1;  // floor
   bool in;              // lower corner inside the grid (cell path), else the 8-tap gather
-  float qb;             // brick bound as q*bq (255*bq: no bound); two-level sparse: the macro bound
-  const float4* cp;     // the cell's two float4 (valid when in && m.cells; two-level: after woodcock_refine)
-  uint32_t fi, loc;     // two-level sparse: index of the brick word, cell within its leaf
+  float qb;             // brick bound (bound_value; 1.9375: no bound)
+  const float4* cp;     // the cell's two float4 (valid when in && m.cells)
 };
 CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t) {
   WoodcockPoint P;
@@ -502,46 +497,24 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
   // above +inf, and cx is never -0 (above).  One compare per axis, one mask.
   P.in = ((int)(det_f2u(P.cx) < det_f2u(m.fres_x)) & (int)(det_f2u(P.cy) < det_f2u(m.fres_y)) &
           (int)(det_f2u(P.cz) < det_f2u(m.fres_z))) != 0;
-  const uint32_t x1 = P.in ? (uint32_t)P.fx1 : 0u, y1 = P.in ? (uint32_t)P.fy1 : 0u,
-                 z1 = P.in ? (uint32_t)P.fz1 : 0u;
-  // 24-bit multiplies: the host keeps bnx*bny, rx*ry and ry*rz below 2^24
+  // The cell and brick indices only mean something when in: off the grid the
+  // brick index is replaced by the sentinel entry (no bound) and the cell
+  // pointer is never used (the 8-tap gather).  24-bit multiplies: the host
+  // keeps bnx*bny, rx*ry and ry*rz below 2^24.
+  const uint32_t x1 = (uint32_t)P.fx1, y1 = (uint32_t)P.fy1, z1 = (uint32_t)P.fz1;
   const uint32_t bx = x1 >> m.bshift, by = y1 >> m.bshift, bz = z1 >> m.bshift;
-  const uint32_t bi = __umul24(bz, m.bnxy) + __umul24(by, m.bnx) + bx;
-  // x1 = y1 = z1 = 0 when !in, so bi is a valid index either way: the bound
-  // is loaded unconditionally and replaced afterwards (no branch)
-  if (m.scoarse) {  // two-level sparse: the macro word now, the brick word in woodcock_refine
-    const uint32_t cw = m.scoarse[__umul24(bz >> 2, m.cnxy) + __umul24(by >> 2, m.cnx) + (bx >> 2)];
-    const uint32_t e = P.in ? cw : 0xFF000000u;
-    P.qb = (float)(e >> 24) * m.bq;
-    P.fi = ((e & 0xFFFFFFu) << 6) | ((bz & 3u) << 4) | ((by & 3u) << 2) | (bx & 3u);
-    P.loc = leaf_local(x1, y1, z1);
-    P.cp = m.cells;
-  } else if (m.sbounds) {  // sparse: bound and cell-leaf slot in one word
+  const uint32_t bi = P.in ? __umul24(bz, m.bnxy) + __umul24(by, m.bnx) + bx : m.bsentinel;
+  if (m.sbounds) {  // sparse: bound and cell-leaf slot in one word
     const uint32_t sw = m.sbounds[bi];
-    const uint32_t e = P.in ? sw : 0xFF000000u;
-    P.qb = (float)(e >> 24) * m.bq;
-    P.cp = m.cells + ((((size_t)(e & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
+    P.qb = bound_value(sw >> 24);
+    P.cp = m.cells + ((((size_t)(sw & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
   } else {
     uint32_t q = 255u;
-    if (m.bounds) {
-      const uint32_t qb = m.bounds[bi];
-      q = P.in ? qb : 255u;
-    }
-    P.qb = (float)q * m.bq;
+    if (m.bounds) q = m.bounds[bi];
+    P.qb = bound_value(q);
     P.cp = m.cells + 2 * (__umul24(z1, m.rxy) + __umul24(y1, m.rx) + x1);
   }
   return P;
-}
-// Second level of a two-level sparse bound (after the macro bound failed to
-// bound the point out): the brick word gives the brick bound and the cell.
-// Returns whether the density must be evaluated (!(q*bq < xt)).  Without
-// two-level bounds: true (the first bound was the brick's).
-CVR_DEV bool woodcock_refine(const MediumParams& m, WoodcockPoint& P, float xt) {
-  if (!m.scoarse || !P.in) return true;
-  const uint32_t sw = m.sbounds[P.fi];
-  P.qb = (float)(sw >> 24) * m.bq;
-  P.cp = m.cells + ((((size_t)(sw & 0xFFFFFFu)) << 9 | P.loc) << 1);
-  return !(P.qb < xt);
 }
 // The exact density at the point (cell trilinear or the 8-tap gather).
 CVR_DEV float woodcock_density(const MediumParams& m, const WoodcockPoint& P) {
@@ -565,7 +538,6 @@ CVR_DEV int woodcock_step_core(const MediumParams& m, V3 o, V3 d, float max_t, f
   WoodcockPoint P = woodcock_point(m, o, d, t);
   const float xi_test = rng_float(rng);
   if (P.qb < xi_test) return 0;  // bounded out (brick bound)
-  if (!woodcock_refine(m, P, xi_test)) return 0;
   ++n_fetch;
   const float rho = m.scale * woodcock_density(m, P);
   if (!(rho * m.inv_sigma < xi_test)) return t < max_t ? 2 : 3;

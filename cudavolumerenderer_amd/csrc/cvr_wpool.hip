@@ -385,7 +385,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     m.leaf_density = nullptr;
     m.leaf_albedo = nullptr;
     m.sbounds = nullptr;
-    m.scoarse = nullptr;
     if constexpr (kMed == kMedDenseFull || kMed == kMedDenseFullUniform) {
       __builtin_assume(m.cells != nullptr);
       __builtin_assume(m.bounds != nullptr);
@@ -393,13 +392,12 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     }
   } else {
     // and sparse instances see the dense pointers as constant null (a sparse medium
-    // has leaves, brick words and no dense grids; two-level bounds are a build option)
+    // has leaves, brick words and no dense grids)
     m.density = nullptr;
     m.albedo = nullptr;
     m.bounds = nullptr;
     __builtin_assume(m.leaves != nullptr);
     __builtin_assume(m.sbounds != nullptr);
-    if (!CVR_SPARSE_2LEVEL) m.scoarse = nullptr;
     m.albedo_uniform = 0u;
   }
   static_assert(sizeof(WavePool<kSlots>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
@@ -446,16 +444,19 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     int slot = -1;      // pool slot of the lane's path, -1 = none
     // woodcock_step_core result of the lane's segment: 0 still tracking,
     // 2 real collision, 1/3 boundary (1: the last step evaluated no
-    // density); filed at the next swap
+    // density); filed at the next swap.  The track loop sets 2 for every
+    // accepted point; filing turns an acceptance at t == max_t into 3 (the
+    // reference scatters iff t < max_t), so the step carries no compare for it.
     int fst = 0;
     V3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
     Rng rng{0, 0, 0, 0, 0, 0};
     float t = 0.0f, max_t = 0.0f;
     for (;;) {
-      const unsigned long long trk = __ballot(slot >= 0 && fst == 0);
+      const unsigned long long trk = (__ballot(slot >= 0) & __ballot(fst == 0));
       const uint32_t n_trk = (uint32_t)__popcll(trk);
       // ---- swap: file finished segments, pull track-ready paths ----------
       if (64u - n_trk >= batch || n_trk == 0u) {
+        if (fst == 2 && !(t < max_t)) fst = 3;
         if (fst != 0) store_track(S, (uint32_t)slot, t, rng);
         const unsigned long long mc = __ballot(fst == 2), mb = __ballot(fst & 1);
         if (fst == 2) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
@@ -479,15 +480,16 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
         n_ready -= k;
       }
-      const uint32_t n_act = (uint32_t)__popcll(__ballot(slot >= 0 && fst == 0));
+      const uint32_t n_act = (uint32_t)__popcll((__ballot(slot >= 0) & __ballot(fst == 0)));
       const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0));
       // EVENT next: a full wave of waiting events, slots never filled, or
       // nothing left to track.  Park: tracking lanes return (t, rng) to the
       // pool, finished lanes are filed.  (Once the queues are empty n_ln is a
       // stand-in that lowers this threshold: see the end of the event batch.)
       if (n_lb + n_lc + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
+        if (fst == 2 && !(t < max_t)) fst = 3;
         if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
-        const unsigned long long mr = __ballot(slot >= 0 && fst == 0);
+        const unsigned long long mr = (__ballot(slot >= 0) & __ballot(fst == 0));
         const unsigned long long mc = __ballot(fst == 2), mb = __ballot(fst & 1);
         if (slot >= 0 && fst == 0) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)slot;
         if (fst == 2) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
@@ -516,10 +518,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             fst = 1;
           } else {
             WoodcockPoint P = woodcock_point(m, o, d, t);
-            if (!(P.qb < xt) && woodcock_refine(m, P, xt)) {
+            if (!(P.qb < xt)) {
               ++c_fetch;
               const float rho = m.scale * woodcock_density(m, P);
-              if (!(rho * m.inv_sigma < xt)) fst = t < max_t ? 2 : 3;
+              if (!(rho * m.inv_sigma < xt)) fst = 2;
             }
           }
         }
