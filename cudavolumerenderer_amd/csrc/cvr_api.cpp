@@ -239,16 +239,18 @@ int wpool_waves_for(const cvr_ctx* c, bool sparse) {
 // ramp-down at the full grid: half the grid alone, a quarter with renders in
 // flight (the other renders fill the rest; profiles/round2/overlap_c1.log:
 // 0.228 vs 0.287 ms alone, 0.094 vs 0.149 ms per render with three in flight).
-// With renders in flight (CVR_OPT_INFLIGHT > 1) a launch of fewer than 1024
-// paths per wave (an 8-GPU block shard of C2) takes half the grid, so each
-// wave gets twice the paths (1/8 shard 0.700 vs 0.735 ms per render,
-// profiles/round2/overlap_small_shards.log); alone the full grid is faster.
+// With renders in flight (CVR_OPT_INFLIGHT > 1) a launch of fewer than 2048
+// paths per wave at the full grid (the 8- and 4-GPU block shards of C2) takes
+// half the grid, so each wave gets twice the paths (1/8 shard 0.700 vs 0.735
+// ms per render, profiles/round2/overlap_small_shards.log; round 4, three in
+// flight: 1/4 shard 1.282 vs 1.320 ms, 1/8 shard 0.724 vs 0.768 at 3/4 grid,
+// profiles/round4/shard_grid.log); alone the full grid is faster.
 uint32_t wpool_launch_grid(const cvr_ctx* c, uint64_t n_paths) {
   if (c->grid_override) return c->grid_override;
   const uint32_t full = (uint32_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
   const uint32_t half = std::max(1u, full / 2), quarter = std::max(1u, full / 4);
   if (n_paths < 64ull * full) return c->inflight > 1 ? quarter : half;
-  if (c->inflight > 1 && n_paths < 1024ull * full) return half;
+  if (c->inflight > 1 && n_paths < 2048ull * full) return half;
   return full;
 }
 
