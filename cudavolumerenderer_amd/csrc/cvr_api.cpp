@@ -1262,14 +1262,23 @@ int cvr_launch_render(cvr_ctx* c) {
   c->last_iterations = 0;
   c->last_track_ms = c->last_events_ms = 0;
   if (c->rng_binding == 1) {
-    if (c->kernel != CVR_KERNEL_REGENERATION_SK)
-      return set_err(&c->err, CVR_ERR_UNSUPPORTED, "thread-bound RNG (CVR_OPT_RNG_BINDING 1) is regenerationSK only");
-    if (L.order) {  // one queue of path ids in order: the thread-bound kernel has no work bands
+    if (c->kernel != CVR_KERNEL_REGENERATION_SK && c->kernel != CVR_KERNEL_STREAMING_SK &&
+        c->kernel != CVR_KERNEL_SORTING_SK)
+      return set_err(&c->err, CVR_ERR_UNSUPPORTED,
+                     "thread-bound RNG (CVR_OPT_RNG_BINDING 1) is regenerationSK, streamingSK or sortingSK only");
+    if (L.order) {  // one queue of path ids in order: the thread-bound kernels have no work bands
       L.order = 0;
       L.n_queues = 1;
     }
-    const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 16u;
-    HIP_TRY(c, cvr::launch_regen_thread(launch_medium(c), L, eps, grid, c->stream));
+    if (c->kernel == CVR_KERNEL_REGENERATION_SK) {
+      const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 16u;
+      HIP_TRY(c, cvr::launch_regen_thread(launch_medium(c), L, eps, grid, c->stream));
+    } else {
+      // StreamingVolPTsk / SortingVolPTsk: 256-thread blocks, the occupancy grid (maxOccupancyGrid,
+      // RenderKernelLauncher.cu:501-508) of 2 blocks per CU unless CVR_OPT_GRID says otherwise
+      const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 2u;
+      HIP_TRY(c, cvr::launch_stream_thread(launch_medium(c), L, c->kernel == CVR_KERNEL_SORTING_SK, grid, c->stream));
+    }
   } else if (c->kernel == CVR_KERNEL_NAIVE_SK) {
     HIP_TRY(c, cvr::launch_naive(launch_medium(c), L, eps, c->stream));
   } else if (c->kernel == CVR_KERNEL_NAIVE_MK && c->mk_compaction) {

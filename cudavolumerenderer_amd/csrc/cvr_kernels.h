@@ -62,6 +62,9 @@ uint32_t wpool_slots(int waves, bool sparse);
 // `grid` one-wave workgroups, path ids from the launch's single queue head.
 hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,
                                hipStream_t s);
+// streamingSK / sortingSK with the thread-bound RNG (CVR_OPT_RNG_BINDING 1): blocks of 256 threads
+hipError_t launch_stream_thread(const MediumParams& m, const LaunchParams& L, bool sorting, uint32_t grid,
+                                hipStream_t s);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
 // naiveMK with the reference's compaction count (CVR_OPT_MK_COMPACTION 1):
 // d_init over the tile's pixels, then one d_extend launch per bounce; `st`

@@ -322,6 +322,188 @@ __global__ __launch_bounds__(64) void k_regen_thread(MediumParams m, LaunchParam
   flush_stats(L, c);
 }
 
+// StreamingVolPTsk / SortingVolPTsk (StreamingVolPTsk_kernel.cuh:328-349,
+// SortingVolPTsk_kernel.cuh:306-330) with the reference's thread-bound RNG
+// (CVR_OPT_RNG_BINDING 1): blocks of 256 threads
+// (STREAMING_THREADS_BLOCK, one item per thread), thread tid owning
+// Rng(seed + tid) (:341) for whichever path it holds; every iteration the
+// block regenerates the threads past n_active, extends every active path
+// (streamingSK: one segment, or until the path ends once the head has passed
+// n_paths; sortingSK: one segment with the collision's albedo deferred past
+// the roulette while paths remain, else until the path ends) and compacts by a
+// stable Morton sort of the ray origins (MortonSort.h:28-49): the paths move
+// between threads, the RNG streams do not.  The oracle's
+// oracle_render_stream_thread_bound restates one block in lockstep:
+// regeneration reads the head once and hands out ids in thread order (one
+// atomic per block here), so a one-block launch is deterministic; with more
+// blocks the assignment depends on timing, as in the reference.
+constexpr uint32_t kStreamThreads = 256;
+__device__ __forceinline__ uint32_t lane_rank64(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint32_t expand_bits10(uint32_t v) {  // Utilities.h:35-41
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+__device__ __forceinline__ uint32_t morton3d_ref(float x, float y, float z) {  // Utilities.h:45-55
+  x = det_fminf(det_fmaxf(x * 1024.0f, 0.0f), 1023.0f);
+  y = det_fminf(det_fmaxf(y * 1024.0f, 0.0f), 1023.0f);
+  z = det_fminf(det_fmaxf(z * 1024.0f, 0.0f), 1023.0f);
+  return expand_bits10((uint32_t)x) * 4u + expand_bits10((uint32_t)y) * 2u + expand_bits10((uint32_t)z);
+}
+template <bool kSorting>
+__global__ __launch_bounds__(256) void k_stream_thread(MediumParams m, LaunchParams L) {
+  __shared__ unsigned long long s_key[kStreamThreads];
+  __shared__ float s_f[9][kStreamThreads];  // o, d, T of the threads' paths (the swap)
+  __shared__ uint32_t s_u[3][kStreamThreads];  // image_id, nseg, texture_access
+  __shared__ uint32_t s_wave[4], s_base, s_head;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  PathState ps;
+  rng_init(ps.rng, (int32_t)(L.seed_base + blockIdx.x * kStreamThreads + tid));  // Rng(c_seed + gtid), Q3
+  ps.o = ps.d = ps.T = mk3(0, 0, 0);
+  ps.image_id = 0;
+  uint32_t nseg = 0, n_active = 0;
+  const V3 ext = sub3(m.bmax, m.bmin);
+  for (;;) {
+    // ---- regenerate (StreamingVolPTsk_kernel.cuh:66-105): the head read once for the block
+    const bool req = tid >= n_active;
+    const unsigned long long rq = __ballot(req);
+    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(rq);
+    __syncthreads();
+    uint32_t before = 0, n_req = 0;
+    for (uint32_t w = 0; w < 4u; ++w) {
+      before += w < wave ? s_wave[w] : 0u;
+      n_req += s_wave[w];
+    }
+    if (tid == 0) {
+      const uint32_t h = __hip_atomic_load(L.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_base = h < L.path_count ? atomicAdd(L.queue, n_req) : 0xFFFFFFFFu;
+      s_head = __hip_atomic_load(L.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const uint32_t base = s_base;
+    bool active = true;
+    if (req) {
+      const uint32_t h = base + before + lane_rank64(rq);
+      if (base == 0xFFFFFFFFu || h >= L.path_count) {
+        active = false;
+      } else {
+        const uint32_t path_id = L.path_first + h;
+        ps.image_id = path_id - fastdiv(path_id, L.div_tile_px) * L.tile_px;
+        camera_ray(L, ps);  // from the thread's stream
+        nseg = 0;
+        ++c[STAT_PATHS];
+      }
+    }
+    // ---- extend
+    const bool should_regenerate = s_head <= L.path_count;  // sortingSK, once per extend (:193)
+    bool texacc = false;
+    if (active) {
+      do {
+        if (L.max_segments && nseg >= L.max_segments) {  // safety cap, as the path-bound walk
+          ++c[STAT_TRUNCATED];
+          active = false;
+          break;
+        }
+        ++nseg;
+        ++c[STAT_SEGMENTS];
+        Isect is;  // a fresh SimpleIsect per segment
+        is.dist = 0.0f;
+        is.normal = mk3(0, 0, 0);
+        is.inside = false;
+        if (!aabb_intersect(m, ps.o, ps.d, is)) {
+          splat(L, ps);
+          ++c[STAT_ESCAPED];
+          active = false;
+        } else {
+          float t = 0.0f;
+          bool collided = false;
+          if (is.inside) {
+            int r;
+            do {
+              r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
+            } while (r == 0);
+            collided = t < is.dist;
+          }
+          if (!collided) {
+            boundary_event(m, ps, is);
+          } else {
+            ps.o = sub3(add3(ps.o, scl3(ps.d, t)), scl3(ps.d, CVR_EPSILON_F));
+            ++c[STAT_ALBEDO];
+            if (kSorting && should_regenerate) {
+              texacc = true;  // delayed texture access (SortingVolPTsk_kernel.cuh:230-237)
+            } else {
+              ps.T = mul3(ps.T, albedo_lookup(m, div3(sub3(ps.o, m.bmin), ext)));
+            }
+            const float e1 = rng_float(ps.rng);
+            const float e2 = rng_float(ps.rng);
+            ps.d = hg_sample(ps.d, m.g, e1, e2);
+          }
+        }
+        // roulette after every segment, an escape included, T / p either way
+        const float p = det_fminf(1.0f, det_fmaxf(det_fmaxf(ps.T.x, ps.T.y), ps.T.z));
+        if (rng_float(ps.rng) > p) active = false;
+        ps.T = mk3(ps.T.x / p, ps.T.y / p, ps.T.z / p);
+      } while ((kSorting ? !should_regenerate
+                         : __hip_atomic_load(L.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > L.path_count) &&
+               active);
+    }
+    // ---- compaction: stable Morton sort of the origins (inactive: morton3D(1,1,1) = 2^30 - 1)
+    uint32_t code = 0x3FFFFFFFu;
+    if (active) {
+      const V3 q = div3(sub3(ps.o, m.bmin), ext);  // AABB::transform
+      code = morton3d_ref(q.x, q.y, q.z);
+    }
+    s_key[tid] = ((unsigned long long)code << 10) | tid;
+    const unsigned long long am = __ballot(active);
+    __syncthreads();
+    if (lane == 0) s_wave[wave] = (uint32_t)__popcll(am);
+    for (uint32_t k = 2; k <= kStreamThreads; k <<= 1) {  // bitonic sort of 256 unique keys
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        const uint32_t ix = tid ^ j;
+        if (ix > tid) {
+          const unsigned long long a = s_key[tid], b = s_key[ix];
+          if (((tid & k) == 0) == (a > b)) {
+            s_key[tid] = b;
+            s_key[ix] = a;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    n_active = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    // swap (SortingVolPTsk_kernel.cuh:105-146): the path of thread key[tid] & 1023 moves here
+    s_f[0][tid] = ps.o.x;
+    s_f[1][tid] = ps.o.y;
+    s_f[2][tid] = ps.o.z;
+    s_f[3][tid] = ps.d.x;
+    s_f[4][tid] = ps.d.y;
+    s_f[5][tid] = ps.d.z;
+    s_f[6][tid] = ps.T.x;
+    s_f[7][tid] = ps.T.y;
+    s_f[8][tid] = ps.T.z;
+    s_u[0][tid] = ps.image_id;
+    s_u[1][tid] = nseg;
+    s_u[2][tid] = texacc ? 1u : 0u;
+    __syncthreads();
+    const uint32_t src = (uint32_t)(s_key[tid] & 1023u);
+    ps.o = mk3(s_f[0][src], s_f[1][src], s_f[2][src]);
+    ps.d = mk3(s_f[3][src], s_f[4][src], s_f[5][src]);
+    ps.T = mk3(s_f[6][src], s_f[7][src], s_f[8][src]);
+    ps.image_id = s_u[0][src];
+    nseg = s_u[1][src];
+    if (kSorting && s_u[2][src]) ps.T = mul3(ps.T, albedo_lookup(m, div3(sub3(ps.o, m.bmin), ext)));
+    if (tid == 0) s_head = __hip_atomic_load(L.queue, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (n_active == 0u && s_head >= L.path_count) break;  // block-uniform (:349)
+  }
+  flush_stats(L, c);
+}
+
 // ----------------------------------------------------- image transfer -----
 // Intended semantics of HostImageBufferTansferDelegate::transfer
 // (ImageBufferTransfer.cu:61-78, fixed per SURVEY Q10): image[off + p] =
@@ -561,6 +743,16 @@ hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatt
     hipLaunchKernelGGL(k_trace<true>, dim3(grid), dim3(256), 0, s, m, L, rec);
   else
     hipLaunchKernelGGL(k_trace<false>, dim3(grid), dim3(256), 0, s, m, L, rec);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_thread(const MediumParams& m, const LaunchParams& L, bool sorting, uint32_t grid,
+                                hipStream_t s) {
+  if (L.path_count == 0) return hipSuccess;
+  if (sorting)
+    hipLaunchKernelGGL(k_stream_thread<true>, dim3(grid), dim3(kStreamThreads), 0, s, m, L);
+  else
+    hipLaunchKernelGGL(k_stream_thread<false>, dim3(grid), dim3(kStreamThreads), 0, s, m, L);
   return hipGetLastError();
 }
 

@@ -87,9 +87,15 @@ typedef enum {
                                  deterministic, scheduler-independent); 1 the reference's binding,
                                  Rng(seed + tid) per persistent thread, roulette draw after an
                                  escape, isect kept across a thread's paths
-                                 (RegenerationVolPTsk_kernel.cuh:146-232).  Thread-bound results
+                                 (RegenerationVolPTsk_kernel.cuh:146-232).  streamingSK / sortingSK:
+                                 1 runs the reference's block scheduler, 256-thread blocks with
+                                 Rng(seed + gtid) per thread, one segment per iteration and a
+                                 stable Morton-sort compaction that moves paths between threads
+                                 (StreamingVolPTsk_kernel.cuh:328-349, SortingVolPTsk_kernel.cuh
+                                 :306-330, its deferred albedo included).  Thread-bound results
                                  depend on which thread takes which path: deterministic only for a
-                                 one-wave launch (CVR_OPT_GRID 1). */
+                                 one-wave (regenerationSK) or one-block (streaming/sorting) launch,
+                                 CVR_OPT_GRID 1. */
   CVR_OPT_MORTON = 17,         /* pool scheduler (streamingSK): 1 sorts each track phase's paths by the
                                  Morton code of their origin in the box (MortonSort.h:28-49,
                                  StreamingVolPTsk_kernel.cuh:188-216); default 0 (measured slower

@@ -944,6 +944,205 @@ EXPORT int oracle_render_thread_bound(const oracle_medium* m, const oracle_launc
   return 0;
 }
 
+/* ------------------------------- thread-bound streamingSK / sortingSK -- */
+/* StreamingVolPTsk_kernel::BlockStreamingVolPT::render (StreamingVolPTsk_kernel.cuh
+ * :328-349; kSortingRays, the variant d_render defaults to, :373-381) and
+ * SortingVolPTsk_kernel::BlockSortingVolPT::render (SortingVolPTsk_kernel.cuh
+ * :306-330) with the reference's RNG binding (CVR_OPT_RNG_BINDING 1):
+ * one block of n_threads threads (STREAMING_THREADS_BLOCK = 256, Defines.h:21,
+ * ITEMS_PER_THREAD 1), thread tid owning Rng(seed + tid) (:341) for whatever
+ * path it holds; a path moves between threads at every compaction, its RNG
+ * does not.  One iteration of the block:
+ *   - regenerate (:66-105): every thread is active; a thread with tid >=
+ *     n_active takes a new path unless the head has reached n_paths.  Restated
+ *     in lockstep: the head is read once, the requesting threads take
+ *     consecutive ids in thread order and the head advances by their number
+ *     (so it can pass n_paths, as it does when a warp's atomics race);
+ *   - extend: each active thread runs segments (fresh SimpleIsect, scatter at
+ *     o + d t - d eps, roulette after every segment, an escape included) until
+ *     its path ends or, streamingSK (:284-286), while head > n_paths; sortingSK
+ *     (:193-277) decides once per extend, should_regenerate = head <= n_paths:
+ *     then it runs one segment per iteration and a collision defers its albedo
+ *     (texture_access) past the roulette, otherwise it loops and multiplies
+ *     the albedo at once;
+ *   - compaction (MortonSort.h:28-49, :188-216): keys = 30-bit Morton code of
+ *     the ray origin in the box (AABB::transform, morton3D, Utilities.h:35-55),
+ *     morton3D(1,1,1) for inactive threads; a stable sort (cub BlockRadixSort)
+ *     gives thread j the path of the thread holding the j-th smallest key;
+ *     n_active = the number of active threads; sortingSK then applies each
+ *     deferred albedo at the moved path's origin (:118-124).
+ * The block loops while n_active > 0 || head < n_paths (:349). */
+typedef struct {
+  xorwow_t rng;
+  f3 o, d, T;
+  uint32_t image_id, nseg;
+  int active, texacc;
+} st_thread_t;
+
+static uint32_t expand_bits10(uint32_t v) { /* Utilities.h:35-41 */
+  v = (v * 0x00010001u) & 0xFF0000FFu;
+  v = (v * 0x00000101u) & 0x0F00F00Fu;
+  v = (v * 0x00000011u) & 0xC30C30C3u;
+  v = (v * 0x00000005u) & 0x49249249u;
+  return v;
+}
+static uint32_t morton3d(float x, float y, float z) { /* Utilities.h:45-55 */
+  x = det_fminf(det_fmaxf(x * 1024.0f, 0.0f), 1023.0f);
+  y = det_fminf(det_fmaxf(y * 1024.0f, 0.0f), 1023.0f);
+  z = det_fminf(det_fmaxf(z * 1024.0f, 0.0f), 1023.0f);
+  return expand_bits10((uint32_t)x) * 4u + expand_bits10((uint32_t)y) * 2u + expand_bits10((uint32_t)z);
+}
+static int cmp_u64(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+
+EXPORT int oracle_render_stream_thread_bound(const oracle_medium* m, const oracle_launch* L, uint32_t n_threads,
+                                             uint32_t first, uint32_t count, int sorting, float* out,
+                                             oracle_stats* stats) {
+  if (n_threads == 0 || n_threads > 1024) return -1;
+  st_thread_t* th = (st_thread_t*)calloc(n_threads, sizeof(st_thread_t));
+  st_thread_t* tmp = (st_thread_t*)calloc(n_threads, sizeof(st_thread_t));
+  uint64_t* key = (uint64_t*)calloc(n_threads, sizeof(uint64_t));
+  if (!th || !tmp || !key) {
+    free(th);
+    free(tmp);
+    free(key);
+    return -1;
+  }
+  oracle_stats st;
+  memset(&st, 0, sizeof(st));
+  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
+  const f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
+  const f3 bmax = mk3(m->box_max[0], m->box_max[1], m->box_max[2]);
+  const uint32_t code_max = morton3d(1.0f, 1.0f, 1.0f);
+  for (uint32_t t = 0; t < n_threads; ++t) rng_init(&th[t].rng, (int32_t)(L->seed_base + t)); /* Q3 */
+  uint32_t head = 0, n_active = 0;
+  do {
+    /* regenerate */
+    const uint32_t h0 = head;
+    uint32_t req = 0;
+    for (uint32_t t = 0; t < n_threads; ++t) {
+      st_thread_t* p = &th[t];
+      p->active = 1;
+      if (t < n_active) continue;
+      if (h0 >= count) {
+        p->active = 0;
+        continue;
+      }
+      const uint32_t h = h0 + req++;
+      if (h >= count) {
+        p->active = 0;
+        continue;
+      }
+      const uint32_t path_id = first + h;
+      p->image_id = path_id % tile_px;
+      float px = (float)(p->image_id % (uint32_t)L->tile_res[0]) + (float)L->offset[0];
+      float py = det_floorf((float)p->image_id / L->tile_res[0]) + (float)L->offset[1];
+      camera_ray(L, px, py, &p->rng, &p->o, &p->d);
+      p->T = mk3(1.0f, 1.0f, 1.0f);
+      p->nseg = 0;
+      st.paths++;
+    }
+    if (h0 < count) head = h0 + req;
+    /* extend */
+    const int should_regenerate = head <= count; /* sortingSK, read once per extend */
+    for (uint32_t t = 0; t < n_threads; ++t) {
+      st_thread_t* p = &th[t];
+      p->texacc = 0;
+      if (!p->active) continue;
+      do {
+        if (L->max_segments && p->nseg >= L->max_segments) { /* safety cap, as the path-bound walk */
+          st.truncated++;
+          p->active = 0;
+          break;
+        }
+        p->nseg++;
+        st.segments++;
+        isect_t is;
+        is.dist = 0.0f;
+        is.normal = mk3(0, 0, 0);
+        is.inside = 0;
+        if (!aabb_intersect(m, p->o, p->d, &is)) {
+          float* px = out + 4 * (size_t)p->image_id; /* atomicVectorAdd(T * Le), Le = 1 */
+          px[0] += p->T.x;
+          px[1] += p->T.y;
+          px[2] += p->T.z;
+          px[3] = 1.0f;
+          st.escaped++;
+          p->active = 0;
+        } else {
+          float sampled = 0.0f;
+          int collided = 0;
+          uint32_t ns = 0, nd = 0;
+          if (is.inside) {
+            sampled = woodcock(m, p->o, p->d, is.dist, &p->rng, &ns, &nd, L->world_to_aabb);
+            collided = sampled < is.dist;
+          }
+          st.steps += ns;
+          st.density += nd;
+          if (!collided) {
+            frame_t fr = frame_from_z(is.normal);
+            f3 dir = frame_to_local(&fr, normalize3(neg3(p->d)));
+            p->o = add3(p->o, scl3(p->d, is.dist));
+            float weight = 1.0f;
+            if (ggx_sample(m, dir, &p->rng, &p->d, &weight)) {
+              p->T = scl3(p->T, weight);
+              p->d = frame_to_world(&fr, p->d);
+              p->o = add3(p->o, scl3(p->d, EPS));
+            }
+          } else {
+            p->o = sub3(add3(p->o, scl3(p->d, sampled)), scl3(p->d, EPS));
+            st.albedo++;
+            if (sorting && should_regenerate) {
+              p->texacc = 1; /* delayed texture access (SortingVolPTsk_kernel.cuh:230-237) */
+            } else {
+              p->T = mul3(p->T, albedo_lookup(m, div3(sub3(p->o, bmin), sub3(bmax, bmin))));
+            }
+            float e1 = rng_float(&p->rng);
+            float e2 = rng_float(&p->rng);
+            p->d = hg_sample(p->d, m->g, e1, e2);
+          }
+        }
+        /* roulette: after every segment, an escape included; T / p either way */
+        float q = det_fminf(1.0f, det_fmaxf(det_fmaxf(p->T.x, p->T.y), p->T.z));
+        if (rng_float(&p->rng) > q) p->active = 0;
+        p->T = mk3(p->T.x / q, p->T.y / q, p->T.z / q);
+      } while ((sorting ? !should_regenerate : head > count) && p->active);
+    }
+    /* compaction: stable Morton sort of the threads' paths, RNGs stay */
+    n_active = 0;
+    for (uint32_t t = 0; t < n_threads; ++t) {
+      const st_thread_t* p = &th[t];
+      uint32_t code = code_max;
+      if (p->active) {
+        const f3 c = div3(sub3(p->o, bmin), sub3(bmax, bmin)); /* AABB::transform */
+        code = morton3d(c.x, c.y, c.z);
+        n_active++;
+      }
+      key[t] = ((uint64_t)code << 10) | t;
+    }
+    qsort(key, n_threads, sizeof(uint64_t), cmp_u64);
+    memcpy(tmp, th, n_threads * sizeof(st_thread_t));
+    for (uint32_t j = 0; j < n_threads; ++j) {
+      const st_thread_t* src = &tmp[key[j] & 1023u];
+      st_thread_t* dst = &th[j];
+      dst->o = src->o;
+      dst->d = src->d;
+      dst->T = src->T;
+      dst->image_id = src->image_id;
+      dst->nseg = src->nseg;
+      if (sorting && src->texacc) /* the deferred albedo at the moved path's origin */
+        dst->T = mul3(dst->T, albedo_lookup(m, div3(sub3(dst->o, bmin), sub3(bmax, bmin))));
+    }
+  } while (n_active > 0 || head < count);
+  free(th);
+  free(tmp);
+  free(key);
+  if (stats) *stats = st;
+  return 0;
+}
+
 /* ----------------------------------------------------- unit probes ----- */
 /* Small entry points used by the known-answer tests. */
 EXPORT void oracle_rng_stream(int32_t seed, uint32_t n, uint32_t* out_u32, float* out_f) {
