@@ -474,7 +474,6 @@ CVR_DEV bool aabb_intersect(const MediumParams& m, V3 o, V3 d, Isect& is) {
 struct WoodcockPoint {
   V3 c;                 // worldToAABB coordinate (Q4)
   float cx, cy, cz;     // grid coordinate (DeviceVolume::volumeToGrid)
-  float fx1, fy1, fz1;  // floor
   bool in;              // lower corner inside the grid (cell path), else the 8-tap gather
   float qb;             // brick bound (bound_value; 1.9375: no bound)
   const float4* cp;     // the cell's two float4 (valid when in && m.cells)
@@ -488,9 +487,6 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
   P.cx = det_fmaf(P.c.x, m.gx, 0.0f);
   P.cy = det_fmaf(P.c.y, m.gy, 0.0f);
   P.cz = det_fmaf(P.c.z, m.gz, 0.0f);
-  P.fx1 = __builtin_floorf(P.cx);
-  P.fy1 = __builtin_floorf(P.cy);
-  P.fz1 = __builtin_floorf(P.cz);
   // floor(cx) >= 0 && floor(cx) < res  <=>  0 <= cx < res (res an integer)
   // <=>  bits(cx) < bits(res) as unsigned: non-negative floats order as
   // their bit patterns, negatives and -NaN have the sign bit set, +NaN lies
@@ -499,9 +495,10 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
           (int)(det_f2u(P.cz) < det_f2u(m.fres_z))) != 0;
   // The cell and brick indices only mean something when in: off the grid the
   // brick index is replaced by the sentinel entry (no bound) and the cell
-  // pointer is never used (the 8-tap gather).  24-bit multiplies: the host
-  // keeps bnx*bny, rx*ry and ry*rz below 2^24.
-  const uint32_t x1 = (uint32_t)P.fx1, y1 = (uint32_t)P.fy1, z1 = (uint32_t)P.fz1;
+  // pointer is never used (the 8-tap gather).  In the grid 0 <= cx < 2^24, so
+  // the truncating conversion is floor(cx) (Volume.h:52, (int)floorf) with no
+  // v_floor.  24-bit multiplies: the host keeps bnx*bny, rx*ry and ry*rz below 2^24.
+  const uint32_t x1 = (uint32_t)P.cx, y1 = (uint32_t)P.cy, z1 = (uint32_t)P.cz;
   const uint32_t bx = x1 >> m.bshift, by = y1 >> m.bshift, bz = z1 >> m.bshift;
   const uint32_t bi = P.in ? __umul24(bz, m.bnxy) + __umul24(by, m.bnx) + bx : m.bsentinel;
   if (m.sbounds) {  // sparse: bound and cell-leaf slot in one word
@@ -520,15 +517,18 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
 CVR_DEV float woodcock_density(const MediumParams& m, const WoodcockPoint& P) {
   if (P.in && m.cells) {
     const float4 lo = P.cp[0], hi = P.cp[1];
-    return trilerp_cell(lo, hi, P.cx - P.fx1, P.cy - P.fy1, P.cz - P.fz1);
+    // cx - floorf(cx) (Volume.h:56-58): exact for 0 <= cx, which is what v_fract_f32 returns
+    return trilerp_cell(lo, hi, __builtin_amdgcn_fractf(P.cx), __builtin_amdgcn_fractf(P.cy),
+                        __builtin_amdgcn_fractf(P.cz));
   }
   return density_lookup_gather(m, P.c);
 }
 // == det_logf(det_fmaxf(xi, EPSILON)) * -inv_sigma + t: xi is never NaN and
 // the clamped argument is a normal float, so the NaN and subnormal paths are
-// dropped.
+// dropped, and the clamp is one v_max_f32 (maxnum, which equals det_fmaxf
+// for a non-NaN xi).
 CVR_DEV float woodcock_advance(const MediumParams& m, float xi, float t) {
-  return det_fmaf(-det_logf_normal(xi < CVR_EPSILON_F ? CVR_EPSILON_F : xi), m.inv_sigma, t);
+  return det_fmaf(-det_logf_normal(__builtin_fmaxf(xi, CVR_EPSILON_F)), m.inv_sigma, t);
 }
 
 CVR_DEV int woodcock_step_core(const MediumParams& m, V3 o, V3 d, float max_t, float& t, Rng& rng,
