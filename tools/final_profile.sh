@@ -1,8 +1,8 @@
 #!/bin/bash
 # One measurement pass of the committed build on the GPU box (gpurun):
 # GPU tests, bench lines for C1-C5, rocprofv3 kernel stats (C2, C3, C5), PMC
-# traffic passes (FETCH_SIZE / WRITE_SIZE, separate runs) and the SQ counter
-# groups for C2.  Every step under its own time limit; stops at the first
+# traffic passes (FETCH_SIZE / WRITE_SIZE, separate runs), the VALU issue pass
+# (tools/valu.py) and the SQ counter groups for C2 and C5.  Every step under its own time limit; stops at the first
 # failure.  Output: gpurun_out/final/.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -27,13 +27,18 @@ for sc in manix hetvol cloud; do
   if [ $sc = cloud ]; then S="--steps 2 --warmup 1"; else S="--steps 3 --warmup 1"; fi
   step pmcf_$sc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
   step pmcw_$sc 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
-  cp "$OUT/libcvr.sha256" "$OUT/pmcf_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcw_$sc/"
+  step pmcv_$sc 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
+  cp "$OUT/libcvr.sha256" "$OUT/pmcf_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcw_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcv_$sc/"
 done
 # fold the traffic passes into profiles/traffic.json here too, so the bench lines
 # below (same libcvr.so) carry their measured traffic
 python3 tools/traffic.py "$OUT/pmcf_manix" "$OUT/pmcw_manix" k_wpool_1024x1024_20it > /dev/null &&
   python3 tools/traffic.py "$OUT/pmcf_hetvol" "$OUT/pmcw_hetvol" hetvol_k_wpool_1024x1024_20it > /dev/null &&
   python3 tools/traffic.py "$OUT/pmcf_cloud" "$OUT/pmcw_cloud" cloud_k_wpool_4096x4096_20it > /dev/null || exit 1
+# and the VALU issue (roofline.valu) of each benchmark kernel instance
+python3 tools/valu.py "$OUT/pmcv_manix" k_wpool_1024x1024_20it "k_wpool<false, 5, 2, false, false>" > /dev/null &&
+  python3 tools/valu.py "$OUT/pmcv_hetvol" hetvol_k_wpool_1024x1024_20it "k_wpool<false, 5, 3, false, false>" > /dev/null &&
+  python3 tools/valu.py "$OUT/pmcv_cloud" cloud_k_wpool_4096x4096_20it "k_wpool<false, 5, 1, false, false>" > /dev/null || exit 1
 step c2_bench 200 python3 bench.py --steps 20 --warmup 5
 step c1_bench 200 python3 bench.py --scene bucky --steps 20 --warmup 5
 step c3_bench 200 python3 bench.py --scene hetvol --steps 20 --warmup 5
