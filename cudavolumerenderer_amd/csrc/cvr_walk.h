@@ -478,8 +478,7 @@ struct WoodcockPoint {
   float qb;             // brick bound (bound_value; 1.9375: no bound)
   const float4* cp;     // the cell's two float4 (valid when in && m.cells)
 };
-CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t) {
-  WoodcockPoint P;
+CVR_DEV void woodcock_coords(const MediumParams& m, V3 o, V3 d, float t, WoodcockPoint& P) {
   P.c = sub3(mk3(det_fmaf(t, d.x, o.x), det_fmaf(t, d.y, o.y), det_fmaf(t, d.z, o.z)), m.shift);
   // fma(c, g, +0) is the product c*g rounded once, except that a -0 product
   // becomes +0 (-0 + +0 = +0); the trilinear weights cx - floor(cx) and the
@@ -493,6 +492,10 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
   // above +inf, and cx is never -0 (above).  One compare per axis, one mask.
   P.in = ((int)(det_f2u(P.cx) < det_f2u(m.fres_x)) & (int)(det_f2u(P.cy) < det_f2u(m.fres_y)) &
           (int)(det_f2u(P.cz) < det_f2u(m.fres_z))) != 0;
+}
+CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t) {
+  WoodcockPoint P;
+  woodcock_coords(m, o, d, t, P);
   // The cell and brick indices only mean something when in: off the grid the
   // brick index is replaced by the sentinel entry (no bound) and the cell
   // pointer is never used (the 8-tap gather).  In the grid 0 <= cx < 2^24, so

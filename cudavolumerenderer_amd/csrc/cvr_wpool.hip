@@ -32,6 +32,9 @@
 #ifndef CVR_WPOOL_UNROLL
 #define CVR_WPOOL_UNROLL 4
 #endif
+// Tentative points per lane per Woodcock group (the lookahead below).  The
+// track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
+constexpr int kLook = 2;
 // Wave priorities (s_setprio): the track loop above the event code, so a
 // stepping wave issues its brick-bound and cell loads ahead of the
 // VALU-dense event batches of the other waves on its SIMD (C2: -0.7%).
@@ -500,29 +503,85 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         n_lb += (uint32_t)__popcll(mb);
         break;
       }
-      // ---- one Woodcock step (Utilities.cuh:147-152) ---------------------
+      // ---- Woodcock steps (Utilities.cuh:147-152), two points at a time ----
+      // woodcock_step_core for two consecutive tentative points: a lane takes
+      // all four draws and loads both brick words before it tests either, so
+      // the wave waits for one brick-word latency per two steps, and the two
+      // points' arithmetic interleaves.  The points after the one that ends
+      // the segment (t > max_t or a real collision) are dropped: t is that
+      // point's, and the RNG goes back to the state after its two draws.
+      // XORWOW shifts its five words by one per draw, so that state is two
+      // saved words plus three of the current ones.  A segment that ends
+      // past max_t has drawn its test value too, as in the one-point step
+      // (the boundary event takes that draw back, rng_undo).  Density
+      // evaluations are steps minus the segments that ended past max_t
+      // (counted when filed), so only steps are counted here.  Measured
+      // (profiles/round4/lookahead.md): 2 points -3.5% C2, -3.4% C3, -2.6% C5
+      // against one; 3 or 4 points, or loading the undecided points' cells
+      // before testing, were slower.
 #pragma unroll
-      for (int u = 0; u < CVR_WPOOL_UNROLL; ++u) {
-        // woodcock_step_core with both draws taken up front: a step that
-        // ends past max_t has drawn its test value too, and the boundary
-        // event takes that draw back (rng_undo).  With no draw inside a
-        // branch the RNG words need no per-path merge copies.  Density
-        // evaluations are steps minus the segments that ended past max_t
-        // (counted when filed), so only steps are counted here.
+      for (int u = 0; u < CVR_WPOOL_UNROLL / kLook; ++u) {
         if (slot >= 0 && fst == 0) {
-          ++c_steps;
-          const float xi = rng_float(rng);
-          const float xt = rng_float(rng);
-          t = woodcock_advance(m, xi, t);
-          if (!(t <= max_t)) {
-            fst = 1;
-          } else {
-            WoodcockPoint P = woodcock_point(m, o, d, t);
-            if (!(P.qb < xt)) {
-              ++c_fetch;
-              const float rho = m.scale * woodcock_density(m, P);
-              if (!(rho * m.inv_sigma < xt)) fst = 2;
+          float tk[kLook], xtk[kLook];
+          uint32_t sva[kLook], svb[kLook];  // draw-sequence words 2k+2, 2k+3 (S_{k+1}.v0, v1)
+          WoodcockPoint Pk[kLook];
+          float tt = t;
+#pragma unroll
+          for (int k = 0; k < kLook; ++k) {
+            const float xi = rng_float(rng);
+            xtk[k] = rng_float(rng);
+            sva[k] = rng.v0;
+            svb[k] = rng.v1;
+            tt = woodcock_advance(m, xi, tt);
+            tk[k] = tt;
+          }
+#pragma unroll
+          for (int k = 0; k < kLook; ++k) Pk[k] = woodcock_point(m, o, d, tk[k]);
+          int end = kLook;  // the first point that ends the segment
+#pragma unroll
+          for (int k = 0; k < kLook; ++k) {
+            if (end == kLook) {
+              if (!(tk[k] <= max_t)) {
+                fst = 1;
+                end = k;
+              } else if (!(Pk[k].qb < xtk[k])) {
+                ++c_fetch;
+                const float rho = m.scale * woodcock_density(m, Pk[k]);
+                if (!(rho * m.inv_sigma < xtk[k])) {
+                  fst = 2;
+                  end = k;
+                }
+              }
             }
+          }
+          c_steps += end == kLook ? kLook : end + 1;
+          t = tk[kLook - 1];
+#pragma unroll
+          for (int k = 0; k < kLook - 1; ++k)
+            if (end == k) t = tk[k];
+          if (end < kLook - 1) {
+            uint32_t w[2 * kLook + 5];
+#pragma unroll
+            for (int k = 0; k < kLook - 1; ++k) {
+              w[2 * k + 2] = sva[k];
+              w[2 * k + 3] = svb[k];
+            }
+            w[2 * kLook] = rng.v0;
+            w[2 * kLook + 1] = rng.v1;
+            w[2 * kLook + 2] = rng.v2;
+            w[2 * kLook + 3] = rng.v3;
+            w[2 * kLook + 4] = rng.v4;
+#pragma unroll
+            for (int j = 1; j < kLook; ++j) {
+              if (end + 1 == j) {
+                rng.v0 = w[2 * j];
+                rng.v1 = w[2 * j + 1];
+                rng.v2 = w[2 * j + 2];
+                rng.v3 = w[2 * j + 3];
+                rng.v4 = w[2 * j + 4];
+              }
+            }
+            rng.d -= (uint32_t)(2 * (kLook - 1 - end)) * 362437u;
           }
         }
       }
