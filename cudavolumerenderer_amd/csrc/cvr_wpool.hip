@@ -373,6 +373,9 @@ enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2, kMedDenseFullUnif
 template <bool kScatterEps, int kWaves, int kMed, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr bool kSparse = kMed == kMedSparse;
+  // Sparse media defer their cell fetches to the end of the track iteration
+  // (the lookahead below): C5 -3.0%; the dense instances lose 5-8% with it.
+  constexpr bool kLookDefer = kSparse;
   constexpr int kSlots = PoolSize<kWaves>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
   // branches of the walk code fold away and take no scalar registers.
@@ -450,10 +453,14 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     // density); filed at the next swap.  The track loop sets 2 for every
     // accepted point; filing turns an acceptance at t == max_t into 3 (the
     // reference scatters iff t < max_t), so the step carries no compare for it.
+    // 4 (sparse only): cell fetch pending, resolved to 0 or 2 before the next
+    // swap check.
     int fst = 0;
     V3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
     Rng rng{0, 0, 0, 0, 0, 0};
     float t = 0.0f, max_t = 0.0f;
+    const float4* pcp = nullptr;  // kLookDefer: the pending fetch's cell and test value
+    float pxt = 0.0f;
     for (;;) {
       const unsigned long long trk = (__ballot(slot >= 0) & __ballot(fst == 0));
       const uint32_t n_trk = (uint32_t)__popcll(trk);
@@ -518,7 +525,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       // (counted when filed), so only steps are counted here.  Measured
       // (profiles/round4/lookahead.md): 2 points -3.5% C2, -3.4% C3, -2.6% C5
       // against one; 3 or 4 points, or loading the undecided points' cells
-      // before testing, were slower.
+      // before testing, were slower.  kLookDefer (sparse media): a point the
+      // bound does not settle parks its lane (fst 4, later points dropped as
+      // for an end) and the lane fetches its cell once after the unrolled
+      // groups, so the wave waits for one cell latency per iteration instead
+      // of one per group that needs a cell; the parked lanes idle meanwhile.
 #pragma unroll
       for (int u = 0; u < CVR_WPOOL_UNROLL / kLook; ++u) {
         if (slot >= 0 && fst == 0) {
@@ -545,11 +556,18 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
                 fst = 1;
                 end = k;
               } else if (!(Pk[k].qb < xtk[k])) {
-                ++c_fetch;
-                const float rho = m.scale * woodcock_density(m, Pk[k]);
-                if (!(rho * m.inv_sigma < xtk[k])) {
-                  fst = 2;
+                if constexpr (kLookDefer) {
+                  fst = 4;  // cell fetch pending (after the groups); the lane steps no further
                   end = k;
+                  pcp = Pk[k].cp;
+                  pxt = xtk[k];
+                } else {
+                  ++c_fetch;
+                  const float rho = m.scale * woodcock_density(m, Pk[k]);
+                  if (!(rho * m.inv_sigma < xtk[k])) {
+                    fst = 2;
+                    end = k;
+                  }
                 }
               }
             }
@@ -583,6 +601,16 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             }
             rng.d -= (uint32_t)(2 * (kLook - 1 - end)) * 362437u;
           }
+        }
+      }
+      if constexpr (kLookDefer) {
+        if (fst == 4) {
+          ++c_fetch;
+          WoodcockPoint P;
+          woodcock_coords(m, o, d, t, P);
+          P.cp = pcp;
+          const float rho = m.scale * woodcock_density(m, P);
+          fst = !(rho * m.inv_sigma < pxt) ? 2 : 0;
         }
       }
     }
