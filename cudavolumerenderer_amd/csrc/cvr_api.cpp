@@ -585,6 +585,58 @@ int mk_reference_render(cvr_ctx* c, const cvr::LaunchParams& L) {
   return CVR_OK;
 }
 
+// streamingMK with the thread-bound RNG (CVR_OPT_RNG_BINDING 1):
+// StreamingVolPTmk::launchRender (RenderKernelLauncher.cu:435-470).  Per
+// iteration d_regenerate fills the slots from n_active on, n_active is reset,
+// the slot buffers swap and d_extend runs one segment per active path (all of
+// them once the head has passed the last path) and compacts the survivors;
+// the host reads n_active and the head back, one sync per iteration as the
+// reference.  The RNG states stay with the threads (cvr_kernels.hip
+// k_smk_extend).  Temporary buffers per call: 2 x 3 float4 + 2 flags per slot,
+// 24 bytes of RNG state per thread.
+int smk_thread_render(cvr_ctx* c, const cvr::LaunchParams& L, uint32_t grid) {
+  if (L.path_count == 0) return CVR_OK;
+  const size_t n = (size_t)grid * 256u;
+  const cvr::MediumParams m = launch_medium(c);
+  float4* slots = nullptr;
+  uint8_t* act = nullptr;
+  uint4* st0 = nullptr;
+  uint2* st1 = nullptr;
+  uint32_t* ctl = nullptr;
+  HIP_TRY(c, hipMalloc(&slots, 6 * n * sizeof(float4)));
+  hipError_t e = hipMalloc(&act, 2 * n);
+  if (e == hipSuccess) e = hipMalloc(&st0, n * sizeof(uint4));
+  if (e == hipSuccess) e = hipMalloc(&st1, n * sizeof(uint2));
+  if (e == hipSuccess) e = hipMalloc(&ctl, 2 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), c->stream);  // d_n_active = head = 0
+  cvr::SmkSlots buf[2] = {{slots, slots + n, slots + 2 * n, act}, {slots + 3 * n, slots + 4 * n, slots + 5 * n, act + n}};
+  int cur = 0;  // the buffer d_regenerate writes and the next d_extend reads
+  uint32_t h[2] = {(uint32_t)n, 0u};
+  uint64_t it = 0;
+  int r = CVR_OK;
+  while (e == hipSuccess && (h[0] > 0u || h[1] < L.path_count)) {
+    if (++it > 100000000ull) {
+      r = set_err(&c->err, CVR_ERR_STATE, "thread-bound streamingMK did not finish");
+      break;
+    }
+    e = cvr::launch_smk_regen(L, buf[cur], st0, st1, ctl, grid, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(ctl, 0, sizeof(uint32_t), c->stream);  // d_n_active = 0
+    if (e == hipSuccess) e = cvr::launch_smk_extend(m, L, buf[cur], buf[cur ^ 1], st0, st1, ctl, grid, c->stream);
+    cur ^= 1;
+    if (e == hipSuccess) e = hipMemcpyAsync(h, ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  }
+  c->last_iterations = (uint32_t)it;
+  (void)hipFree(slots);
+  if (act) (void)hipFree(act);
+  if (st0) (void)hipFree(st0);
+  if (st1) (void)hipFree(st1);
+  if (ctl) (void)hipFree(ctl);
+  if (r) return r;
+  if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "thread-bound streamingMK: %s", hipGetErrorString(e));
+  return CVR_OK;
+}
+
 void compute_range(const cvr_ctx* c, uint64_t* first, uint64_t* count) {
   uint64_t f = c->range_first < c->n_paths ? c->range_first : c->n_paths;
   uint64_t n = c->n_paths - f;
@@ -1263,9 +1315,10 @@ int cvr_launch_render(cvr_ctx* c) {
   c->last_track_ms = c->last_events_ms = 0;
   if (c->rng_binding == 1) {
     if (c->kernel != CVR_KERNEL_REGENERATION_SK && c->kernel != CVR_KERNEL_STREAMING_SK &&
-        c->kernel != CVR_KERNEL_SORTING_SK)
+        c->kernel != CVR_KERNEL_SORTING_SK && c->kernel != CVR_KERNEL_STREAMING_MK)
       return set_err(&c->err, CVR_ERR_UNSUPPORTED,
-                     "thread-bound RNG (CVR_OPT_RNG_BINDING 1) is regenerationSK, streamingSK or sortingSK only");
+                     "thread-bound RNG (CVR_OPT_RNG_BINDING 1) is regenerationSK, streamingSK, sortingSK or "
+                     "streamingMK only");
     if (L.order) {  // one queue of path ids in order: the thread-bound kernels have no work bands
       L.order = 0;
       L.n_queues = 1;
@@ -1273,6 +1326,10 @@ int cvr_launch_render(cvr_ctx* c) {
     if (c->kernel == CVR_KERNEL_REGENERATION_SK) {
       const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 16u;
       HIP_TRY(c, cvr::launch_regen_thread(launch_medium(c), L, eps, grid, c->stream));
+    } else if (c->kernel == CVR_KERNEL_STREAMING_MK) {
+      // 256-thread blocks, the occupancy grid of d_extend (RenderKernelLauncher.cu:366-392)
+      const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 2u;
+      if ((r = smk_thread_render(c, L, grid))) return r;
     } else {
       // StreamingVolPTsk / SortingVolPTsk: 256-thread blocks, the occupancy grid (maxOccupancyGrid,
       // RenderKernelLauncher.cu:501-508) of 2 blocks per CU unless CVR_OPT_GRID says otherwise

@@ -65,6 +65,18 @@ hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, boo
 // streamingSK / sortingSK with the thread-bound RNG (CVR_OPT_RNG_BINDING 1): blocks of 256 threads
 hipError_t launch_stream_thread(const MediumParams& m, const LaunchParams& L, bool sorting, uint32_t grid,
                                 hipStream_t s);
+// streamingMK with the thread-bound RNG (CVR_OPT_RNG_BINDING 1): the reference's regenerate /
+// extend pair per iteration of a host loop, 256-thread blocks, one slot per thread.
+struct SmkSlots {
+  float4* a;     // (o, image_id bits)
+  float4* b;     // (d, segments bits)
+  float4* t;     // (T, 0)
+  uint8_t* act;  // path active
+};
+hipError_t launch_smk_regen(const LaunchParams& L, const SmkSlots& out, uint4* st0, uint2* st1, uint32_t* ctl,
+                            uint32_t grid, hipStream_t s);
+hipError_t launch_smk_extend(const MediumParams& m, const LaunchParams& L, const SmkSlots& in, const SmkSlots& out,
+                             uint4* st0, uint2* st1, uint32_t* ctl, uint32_t grid, hipStream_t s);
 hipError_t launch_naive_mk(const MediumParams& m, const LaunchParams& L, hipStream_t s);
 // naiveMK with the reference's compaction count (CVR_OPT_MK_COMPACTION 1):
 // d_init over the tile's pixels, then one d_extend launch per bounce; `st`

@@ -504,6 +504,147 @@ __global__ __launch_bounds__(256) void k_stream_thread(MediumParams m, LaunchPar
   flush_stats(L, c);
 }
 
+// ------------------------------------------- thread-bound streamingMK -----
+// StreamingVolPTmk_kernel::d_regenerate / d_extend (StreamingVolPTmk_kernel.cuh
+// :26-69, :74-253) with the reference's RNG binding (CVR_OPT_RNG_BINDING
+// 1), one kernel each per iteration of the host loop (smk_thread_render,
+// RenderKernelLauncher.cu:435-470).  Slot j = thread j (ITEMS_PER_THREAD 1);
+// a slot's path lives in SmkSlots (o | image_id, d | nseg, T), its RNG state in
+// the thread's `state` entry, which stays with the thread when compaction moves
+// the path.  ctl[0] = n_active (d_n_active), ctl[1] = the path head.
+// Thread order inside a block (the head and the compaction offset taken once
+// per block): the lockstep order of oracle_render_smk_thread_bound.
+__device__ __forceinline__ void block_rank256(bool flag, uint32_t* s_wave, uint32_t& before, uint32_t& total) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const unsigned long long mk = __ballot(flag);
+  if (lane == 0) s_wave[wave] = (uint32_t)__popcll(mk);
+  __syncthreads();
+  before = lane_rank64(mk);
+  total = 0;
+  for (uint32_t w = 0; w < 4u; ++w) {
+    before += w < wave ? s_wave[w] : 0u;
+    total += s_wave[w];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_smk_regen(LaunchParams L, SmkSlots out, uint4* __restrict__ st0,
+                                                   uint2* __restrict__ st1, uint32_t* __restrict__ ctl) {
+  __shared__ uint32_t s_wave[4], s_base;
+  const uint32_t tid = threadIdx.x, j = blockIdx.x * kStreamThreads + tid;
+  const uint32_t n_active = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool req = j >= n_active;
+  uint32_t before, n_req;
+  block_rank256(req, s_wave, before, n_req);
+  if (tid == 0) {
+    const uint32_t h = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_base = h < L.path_count ? atomicAdd(ctl + 1, n_req) : 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (req) {  // no early return: flush_stats reduces over the whole wave
+    const uint32_t base = s_base, h = base + before;
+    if (base == 0xFFFFFFFFu || h >= L.path_count) {
+      out.act[j] = 0;
+    } else {
+      PathState ps;
+      path_begin(L, L.path_first + h, ps);  // Rng(c_seed + path_id) and the camera ray (:55-59)
+      out.a[j] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.image_id));
+      out.b[j] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(0u));
+      out.t[j] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+      out.act[j] = 1;
+      st0[j] = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);  // states[tid] = rng.getState() (:66)
+      st1[j] = make_uint2(ps.rng.v4, ps.rng.d);
+      c[STAT_PATHS] = 1;
+    }
+  }
+  flush_stats(L, c);
+}
+
+__global__ __launch_bounds__(256) void k_smk_extend(MediumParams m, LaunchParams L, SmkSlots in, SmkSlots out,
+                                                    uint4* __restrict__ st0, uint2* __restrict__ st1,
+                                                    uint32_t* __restrict__ ctl) {
+  __shared__ uint32_t s_wave[4], s_start;
+  const uint32_t tid = threadIdx.x, j = blockIdx.x * kStreamThreads + tid;
+  const uint32_t head = __hip_atomic_load(ctl + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t c[STAT_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint4 r0 = st0[j];
+  const uint2 r1 = st1[j];
+  PathState ps;
+  ps.rng = Rng{r0.x, r0.y, r0.z, r0.w, r1.x, r1.y};  // the thread's state, whatever path slot j holds
+  bool active = in.act[j] != 0;
+  uint32_t nseg = 0;
+  ps.o = ps.d = ps.T = mk3(0, 0, 0);
+  ps.image_id = 0;
+  if (active) {
+    const float4 a = in.a[j], b = in.b[j], t = in.t[j];
+    ps.o = mk3(a.x, a.y, a.z);
+    ps.image_id = __float_as_uint(a.w);
+    ps.d = mk3(b.x, b.y, b.z);
+    nseg = __float_as_uint(b.w);
+    ps.T = mk3(t.x, t.y, t.z);
+  }
+  const V3 ext = sub3(m.bmax, m.bmin);
+  if (active) {
+    do {
+      if (L.max_segments && nseg >= L.max_segments) {  // safety cap, as the path-bound walk
+        ++c[STAT_TRUNCATED];
+        active = false;
+        break;
+      }
+      ++nseg;
+      ++c[STAT_SEGMENTS];
+      Isect is;  // a fresh isect per segment (:163)
+      is.dist = 0.0f;
+      is.normal = mk3(0, 0, 0);
+      is.inside = false;
+      if (!aabb_intersect(m, ps.o, ps.d, is)) {
+        splat(L, ps);
+        ++c[STAT_ESCAPED];
+        active = false;
+      } else {
+        float t = 0.0f;
+        bool collided = false;
+        if (is.inside) {
+          int r;
+          do {
+            r = woodcock_step(m, ps.o, ps.d, is.dist, t, ps.rng, c[STAT_STEPS], c[STAT_DENSITY], c[STAT_FETCH]);
+          } while (r == 0);
+          collided = t < is.dist;
+        }
+        if (!collided) {
+          boundary_event(m, ps, is);
+        } else {
+          ps.o = sub3(add3(ps.o, scl3(ps.d, t)), scl3(ps.d, CVR_EPSILON_F));  // - d eps (:194)
+          ++c[STAT_ALBEDO];
+          ps.T = mul3(ps.T, albedo_lookup(m, div3(sub3(ps.o, m.bmin), ext)));
+          const float e1 = rng_float(ps.rng);
+          const float e2 = rng_float(ps.rng);
+          ps.d = hg_sample(ps.d, m.g, e1, e2);
+        }
+      }
+      // roulette after every segment, an escape included, T / p either way (:203-210)
+      const float p = det_fminf(1.0f, det_fmaxf(det_fmaxf(ps.T.x, ps.T.y), ps.T.z));
+      if (rng_float(ps.rng) > p) active = false;
+      ps.T = mk3(ps.T.x / p, ps.T.y / p, ps.T.z / p);
+    } while (head >= L.path_count && active);  // :212-214
+  }
+  // compaction (:218-252): the block's active paths in thread order at an offset taken once
+  uint32_t before, total;
+  block_rank256(active, s_wave, before, total);
+  if (tid == 0) s_start = atomicAdd(ctl, total);
+  __syncthreads();
+  st0[j] = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);  // the state stays with the thread (:241)
+  st1[j] = make_uint2(ps.rng.v4, ps.rng.d);
+  if (active) {
+    const uint32_t k = s_start + before;
+    out.a[k] = make_float4(ps.o.x, ps.o.y, ps.o.z, __uint_as_float(ps.image_id));
+    out.b[k] = make_float4(ps.d.x, ps.d.y, ps.d.z, __uint_as_float(nseg));
+    out.t[k] = make_float4(ps.T.x, ps.T.y, ps.T.z, 0.0f);
+    out.act[k] = 1;
+  }
+  flush_stats(L, c);
+}
+
 // ----------------------------------------------------- image transfer -----
 // Intended semantics of HostImageBufferTansferDelegate::transfer
 // (ImageBufferTransfer.cu:61-78, fixed per SURVEY Q10): image[off + p] =
@@ -753,6 +894,18 @@ hipError_t launch_stream_thread(const MediumParams& m, const LaunchParams& L, bo
     hipLaunchKernelGGL(k_stream_thread<true>, dim3(grid), dim3(kStreamThreads), 0, s, m, L);
   else
     hipLaunchKernelGGL(k_stream_thread<false>, dim3(grid), dim3(kStreamThreads), 0, s, m, L);
+  return hipGetLastError();
+}
+
+hipError_t launch_smk_regen(const LaunchParams& L, const SmkSlots& out, uint4* st0, uint2* st1, uint32_t* ctl,
+                            uint32_t grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_smk_regen, dim3(grid), dim3(kStreamThreads), 0, s, L, out, st0, st1, ctl);
+  return hipGetLastError();
+}
+
+hipError_t launch_smk_extend(const MediumParams& m, const LaunchParams& L, const SmkSlots& in, const SmkSlots& out,
+                             uint4* st0, uint2* st1, uint32_t* ctl, uint32_t grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_smk_extend, dim3(grid), dim3(kStreamThreads), 0, s, m, L, in, out, st0, st1, ctl);
   return hipGetLastError();
 }
 

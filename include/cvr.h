@@ -92,10 +92,14 @@ typedef enum {
                                  Rng(seed + gtid) per thread, one segment per iteration and a
                                  stable Morton-sort compaction that moves paths between threads
                                  (StreamingVolPTsk_kernel.cuh:328-349, SortingVolPTsk_kernel.cuh
-                                 :306-330, its deferred albedo included).  Thread-bound results
+                                 :306-330, its deferred albedo included).  streamingMK: 1 runs the
+                                 reference's regenerate / extend kernel pair per iteration of a host
+                                 loop, a new path's Rng(seed + path_id) becoming its thread's state
+                                 and the states staying with the threads when compaction moves the
+                                 paths (StreamingVolPTmk_kernel.cuh:26-253).  Thread-bound results
                                  depend on which thread takes which path: deterministic only for a
-                                 one-wave (regenerationSK) or one-block (streaming/sorting) launch,
-                                 CVR_OPT_GRID 1. */
+                                 one-wave (regenerationSK) or one-block (streaming/sorting/
+                                 streamingMK) launch, CVR_OPT_GRID 1. */
   CVR_OPT_MORTON = 17,         /* pool scheduler (streamingSK): 1 sorts each track phase's paths by the
                                  Morton code of their origin in the box (MortonSort.h:28-49,
                                  StreamingVolPTsk_kernel.cuh:188-216); default 0 (measured slower

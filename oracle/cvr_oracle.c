@@ -1143,6 +1143,138 @@ EXPORT int oracle_render_stream_thread_bound(const oracle_medium* m, const oracl
   return 0;
 }
 
+/* ------------------------------------- thread-bound streamingMK ------- */
+/* StreamingVolPTmk::launchRender (RenderKernelLauncher.cu:435-470) with its
+ * kernels d_regenerate / d_extend (StreamingVolPTmk_kernel.cuh:26-69,
+ * :74-253) and their RNG binding (CVR_OPT_RNG_BINDING 1): one block
+ * of n_threads threads (STREAMING_THREADS_BLOCK, ITEMS_PER_THREAD 1), slot j
+ * = thread j.  Per iteration:
+ *   - regenerate: every slot j >= n_active takes a new path (unless the head
+ *     has reached n_paths), Rng(seed + path_id) for its camera ray, and that
+ *     RNG becomes thread j's state (states[tid] = rng.getState(), :66);
+ *     lockstep as in oracle_render_stream_thread_bound: the head is read once
+ *     and the requesting slots take consecutive ids in thread order;
+ *   - extend: thread j continues from states[j] whatever path slot j holds;
+ *     an active path runs a segment (scatter at o + d t - d eps, roulette after
+ *     every segment, an escape included, :194, :203-210) and loops while head >= n_paths
+ *     (:212-214); thread j's state is stored back (:241);
+ *   - compaction: the active paths in thread order (BlockScan, :229-252) go to
+ *     slots 0 .. n_active - 1; the states stay with the threads.
+ * The launcher loops while n_active > 0 || head < n_paths (:439). */
+EXPORT int oracle_render_smk_thread_bound(const oracle_medium* m, const oracle_launch* L, uint32_t n_threads,
+                                          uint32_t first, uint32_t count, float* out, oracle_stats* stats) {
+  if (n_threads == 0 || n_threads > 1024) return -1;
+  st_thread_t* sl = (st_thread_t*)calloc(n_threads, sizeof(st_thread_t)); /* slots: path + active */
+  st_thread_t* nx = (st_thread_t*)calloc(n_threads, sizeof(st_thread_t));
+  xorwow_t* state = (xorwow_t*)calloc(n_threads, sizeof(xorwow_t));        /* states[tid] */
+  if (!sl || !nx || !state) {
+    free(sl);
+    free(nx);
+    free(state);
+    return -1;
+  }
+  oracle_stats st;
+  memset(&st, 0, sizeof(st));
+  const uint32_t tile_px = (uint32_t)(L->tile_res[0] * L->tile_res[1]);
+  const f3 bmin = mk3(m->box_min[0], m->box_min[1], m->box_min[2]);
+  const f3 bmax = mk3(m->box_max[0], m->box_max[1], m->box_max[2]);
+  uint32_t head = 0, n_active = 0;
+  do {
+    /* regenerate */
+    const uint32_t h0 = head;
+    uint32_t req = 0;
+    for (uint32_t t = n_active; t < n_threads; ++t) {
+      st_thread_t* p = &sl[t];
+      p->active = 0;
+      if (h0 >= count) continue;
+      const uint32_t h = h0 + req++;
+      if (h >= count) continue;
+      const uint32_t path_id = first + h;
+      p->image_id = path_id % tile_px;
+      float px = (float)(p->image_id % (uint32_t)L->tile_res[0]) + (float)L->offset[0];
+      float py = det_floorf((float)p->image_id / L->tile_res[0]) + (float)L->offset[1];
+      xorwow_t rng;
+      rng_init(&rng, (int32_t)(L->seed_base + path_id)); /* Rng(c_seed + path_id), Q3 */
+      camera_ray(L, px, py, &rng, &p->o, &p->d);
+      state[t] = rng;
+      p->T = mk3(1.0f, 1.0f, 1.0f);
+      p->nseg = 0;
+      p->active = 1;
+      st.paths++;
+    }
+    if (h0 < count) head = h0 + req;
+    /* extend */
+    for (uint32_t t = 0; t < n_threads; ++t) {
+      st_thread_t* p = &sl[t];
+      xorwow_t* rng = &state[t];
+      if (!p->active) continue;
+      do {
+        if (L->max_segments && p->nseg >= L->max_segments) { /* safety cap, as the path-bound walk */
+          st.truncated++;
+          p->active = 0;
+          break;
+        }
+        p->nseg++;
+        st.segments++;
+        isect_t is;
+        is.dist = 0.0f;
+        is.normal = mk3(0, 0, 0);
+        is.inside = 0;
+        if (!aabb_intersect(m, p->o, p->d, &is)) {
+          float* px = out + 4 * (size_t)p->image_id; /* atomicVectorAdd(T * Le), Le = 1 */
+          px[0] += p->T.x;
+          px[1] += p->T.y;
+          px[2] += p->T.z;
+          px[3] = 1.0f;
+          st.escaped++;
+          p->active = 0;
+        } else {
+          float sampled = 0.0f;
+          int collided = 0;
+          uint32_t ns = 0, nd = 0;
+          if (is.inside) {
+            sampled = woodcock(m, p->o, p->d, is.dist, rng, &ns, &nd, L->world_to_aabb);
+            collided = sampled < is.dist;
+          }
+          st.steps += ns;
+          st.density += nd;
+          if (!collided) {
+            frame_t fr = frame_from_z(is.normal);
+            f3 dir = frame_to_local(&fr, normalize3(neg3(p->d)));
+            p->o = add3(p->o, scl3(p->d, is.dist));
+            float weight = 1.0f;
+            if (ggx_sample(m, dir, rng, &p->d, &weight)) {
+              p->T = scl3(p->T, weight);
+              p->d = frame_to_world(&fr, p->d);
+              p->o = add3(p->o, scl3(p->d, EPS));
+            }
+          } else {
+            p->o = sub3(add3(p->o, scl3(p->d, sampled)), scl3(p->d, EPS));
+            st.albedo++;
+            p->T = mul3(p->T, albedo_lookup(m, div3(sub3(p->o, bmin), sub3(bmax, bmin))));
+            float e1 = rng_float(rng);
+            float e2 = rng_float(rng);
+            p->d = hg_sample(p->d, m->g, e1, e2);
+          }
+        }
+        float q = det_fminf(1.0f, det_fmaxf(det_fmaxf(p->T.x, p->T.y), p->T.z));
+        if (rng_float(rng) > q) p->active = 0;
+        p->T = mk3(p->T.x / q, p->T.y / q, p->T.z / q);
+      } while (head >= count && p->active);
+    }
+    /* compaction: the active paths in thread order; the states stay */
+    n_active = 0;
+    for (uint32_t t = 0; t < n_threads; ++t)
+      if (sl[t].active) nx[n_active++] = sl[t];
+    for (uint32_t t = 0; t < n_active; ++t) sl[t] = nx[t];
+  } while (n_active > 0 || head < count);
+  free(sl);
+  free(nx);
+  free(state);
+  if (stats) *stats = st;
+  return 0;
+}
+
 /* ----------------------------------------------------- unit probes ----- */
 /* Small entry points used by the known-answer tests. */
 EXPORT void oracle_rng_stream(int32_t seed, uint32_t n, uint32_t* out_u32, float* out_f) {

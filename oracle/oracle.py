@@ -74,6 +74,10 @@ def load():
                                                       C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_float),
                                                       C.POINTER(OracleStats)]
     lib.oracle_render_stream_thread_bound.restype = C.c_int
+    lib.oracle_render_smk_thread_bound.argtypes = [C.POINTER(OracleMedium), C.POINTER(OracleLaunch), C.c_uint32,
+                                                   C.c_uint32, C.c_uint32, C.POINTER(C.c_float),
+                                                   C.POINTER(OracleStats)]
+    lib.oracle_render_smk_thread_bound.restype = C.c_int
     lib.oracle_render_mk_reference.argtypes = [C.POINTER(OracleMedium), C.POINTER(OracleLaunch), C.c_uint32,
                                                C.POINTER(C.c_float), C.POINTER(OracleStats), P]
     lib.oracle_render_mk_reference.restype = C.c_int
@@ -204,6 +208,20 @@ class Oracle:
         rc = self.lib.oracle_render_stream_thread_bound(C.byref(self.m), C.byref(L), n_threads, first, count,
                                                         int(sorting), out.ctypes.data_as(C.POINTER(C.c_float)),
                                                         C.byref(st))
+        assert rc == 0
+        return out, st
+
+    def render_smk_thread_bound(self, L: OracleLaunch, n_threads: int, first: int, count: int):
+        """streamingMK with the RNG bound to the thread: one block of
+        n_threads lockstep threads, a new path's RNG Rng(seed + path_id) becoming
+        its thread's state, the states staying with the threads when compaction
+        moves the paths (cvr_oracle.c oracle_render_smk_thread_bound).  Returns
+        (tile accumulator, stats)."""
+        w, h = int(L.tile_res[0]), int(L.tile_res[1])
+        out = np.zeros((h, w, 4), np.float32)
+        st = OracleStats()
+        rc = self.lib.oracle_render_smk_thread_bound(C.byref(self.m), C.byref(L), n_threads, first, count,
+                                                     out.ctypes.data_as(C.POINTER(C.c_float)), C.byref(st))
         assert rc == 0
         return out, st
 
