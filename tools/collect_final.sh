@@ -14,7 +14,7 @@ for sc in manix hetvol cloud; do
   python3 tools/valu.py $F/pmcv_$sc $key "$inst" | cut -c1-140
   cp $F/prof_$sc/run_kernel_stats.csv $P/${c}_kernel_stats.csv
   if [ $sc = cloud ]; then sw="3 1"; else sw="10 2"; fi
-  python3 tools/kernel_phases.py $F/prof_$sc/run_kernel_trace.csv k_wpool $sw $P/${c}_kernel_phases.json | grep _ms
+  python3 tools/kernel_phases.py $F/prof_$sc/run_kernel_trace.csv "$inst" $sw $P/${c}_kernel_phases.json | grep _ms
 done
 python3 tools/pmc_summary.py $P/pmc_k_wpool.json k_wpool $F/pmc_a $F/pmc_b $F/pmc_c $F/pmc_d
 python3 tools/pmc_summary.py $P/pmc_k_wpool_cloud.json k_wpool $F/pmc5_a $F/pmc5_b $F/pmc5_c

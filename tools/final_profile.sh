@@ -23,7 +23,8 @@ step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 600 python3 -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider
 for sc in manix hetvol cloud; do
   if [ $sc = cloud ]; then S="--steps 3 --warmup 1"; else S="--steps 10 --warmup 2"; fi
-  step prof_$sc 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- $B --scene $sc $S
+  # no shard emulation in the traced run: tools/kernel_phases.py reads the bench's own launches
+  step prof_$sc 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- $B --no-shard-emulation --scene $sc $S
   if [ $sc = cloud ]; then S="--steps 2 --warmup 1"; else S="--steps 3 --warmup 1"; fi
   step pmcf_$sc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
   step pmcw_$sc 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
