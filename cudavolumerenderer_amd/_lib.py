@@ -124,7 +124,7 @@ def load() -> C.CDLL:
         "cvr_share_medium": (I32, [P, P]),
         "cvr_trace_launch": (I32, [P, P, U64]),
         "cvr_image_to_host": (I32, [P, P, C.c_size_t, C.c_float, P]),
-        "cvr_render_frame": (I32, [P, P, U32, C.POINTER(Stats)]),
+        "cvr_render_frame": (I32, [P, P, C.c_size_t, U32, C.POINTER(Stats)]),
         "cvr_frame_flush_info": (I32, [P, C.POINTER(U32), C.POINTER(U32)]),
         "cvr_blocks_to_host": (I32, [P, P, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_float, P]),
         "cvr_launch_blocks": (I32, [P, P, P, P]),
@@ -506,22 +506,29 @@ class Context:
                      host: bool = True):
         return self.render_tiles(width, height, n_tiles, iterations, 0, 1, device_image, host)
 
-    def render_frame(self, host_ptr: Optional[int] = None, parts: int = 0, stats: bool = True):
+    def render_frame(self, host_ptr: Optional[int] = None, parts: int = 0, stats: bool = True,
+                     host_floats: Optional[int] = None):
         """CudaVolPath::render for one tile (cvr_render_frame): clear, render
         the set resolution / iterations, and the normalised image in host
         memory when it returns, the launch split into `parts` bands whose
         copies overlap the later bands.  host_ptr: a width*height*4 float
         buffer (pinned for asynchronous copies); None returns a new array.
-        stats=False skips the counters (one synchronous read per band)."""
+        stats=False skips the counters (one synchronous read per band).
+        host_floats: the floats host_ptr holds (the library rejects a buffer
+        shorter than the tile; default: exactly the tile, width*height*4)."""
         st = Stats() if stats else None
         img = None
+        w, h = self.resolution  # the library's own tile size (what cvr_render_frame writes)
         if host_ptr is None:
-            w, h = self.resolution  # the library's own tile size (what cvr_render_frame writes)
             if w == 0 or h == 0:
                 raise CvrError(-3, "render_frame: no resolution set")
             img = np.zeros((h, w, 4), np.float32)
             host_ptr = img.ctypes.data
-        self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), parts, C.byref(st) if stats else None))
+            host_floats = img.size
+        if host_floats is None:
+            host_floats = w * h * 4
+        self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), host_floats, parts,
+                                        C.byref(st) if stats else None))
         return img, st
 
     def frame_flush_info(self):

@@ -108,6 +108,8 @@ struct cvr_ctx {
 
   unsigned char* d_work = nullptr;  // queue heads + stats counters (kWork* layout)
   float4* d_pool_T = nullptr;       // wave-pool scheduler: event-only slot part (LaunchParams::pool_T)
+  unsigned char* d_smk = nullptr;   // thread-bound streamingMK: slot buffers, flags, RNG states, counters
+  size_t smk_n = 0;                 // threads d_smk is carved for
   size_t pool_T_n = 0;
   uint32_t n_queues = 8;            // work-order bands (one per XCD)
   uint32_t subqueues = 8;           // wave pool: queues per band (CVR_OPT_SUBQUEUES)
@@ -201,17 +203,24 @@ bool kernel_supported(int k) { return k >= 0 && k < CVR_KERNEL_UNKNOWN; }
 
 // Scheduler that implements each persistent kernel id (results
 // depend only on the kernel id's scatter offset and per-tile seed, quirks
-// Q2/Q6): regenerationSK and sortingSK run the wave-private LDS pool (sorting
-// = event batches sorted by kind), streamingSK the workgroup LDS pool with
-// bulk compaction phases (StreamingVolPTsk's block streaming), streamingMK
-// the multi-kernel wavefront pair (StreamingVolPTmk's device-wide compaction).
+// Q2/Q6, so every id may run on any scheduler).  Round 5: every persistent id
+// runs the wave-private LDS pool by default, its ballot/prefix compaction of
+// finished segments being the streaming kernels' compaction
+// (StreamingVolPTsk_kernel.cuh:176-216, StreamingVolPTmk_kernel.cuh:218-252)
+// at wave granularity; sortingSK's event batches run sorted by kind; naiveSK
+// (one thread per path in the reference, NaiveVolPTsk_kernel.cuh:17-87) runs
+// there too: its image is fixed by its Rng(path_id) streams, scatter -eps and
+// per-tile seeds, not by the thread mapping (C2: 4.5 vs 26.8 ms as one path
+// per work-item).  The structural restatements stay behind CVR_OPT_SCHEDULER:
+// 4 one path per work-item (k_naive, naiveSK's own mapping), 2 the workgroup
+// pool with bulk compaction phases (StreamingVolPTsk's block streaming, 3-4x
+// slower on C2), 1 the multi-kernel wavefront pair (StreamingVolPTmk's
+// device-wide compaction), 0 one path per lane of a persistent wave.  naiveMK
+// always runs its own kernels (k_naive_mk: per-bounce reseeding, Q12).
+constexpr int kSchedPerItem = 4;
 int scheduler_for(const cvr_ctx* c) {
   if (c->scheduler >= 0) return c->scheduler;
-  switch (c->kernel) {
-    case CVR_KERNEL_STREAMING_SK: return 2;
-    case CVR_KERNEL_STREAMING_MK: return 1;
-    default: return 3;
-  }
+  return 3;
 }
 
 // Scatter origin offset per scheduler: every kernel subtracts
@@ -293,10 +302,10 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   const uint64_t P0 = (uint64_t)(uint32_t)((float)c->tile_w * (float)c->tile_h);
   // the persistent schedulers take work units through unit_to_path (pixel-block order); naiveSK/MK
   // and the wavefront pair map launch index -> path id directly
-  const bool queued = c->kernel != CVR_KERNEL_NAIVE_SK && c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 &&
+  const bool queued = c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 && scheduler_for(c) != kSchedPerItem &&
                       c->rng_binding == 0;
   const bool block_order = queued && c->order && P0 && first % P0 == 0 && count % P0 == 0 && count > 0 &&
-                           c->tile_w % 8 == 0 && c->tile_h % 8 == 0;
+                           count / P0 <= (1ull << 20) && c->tile_w % 8 == 0 && c->tile_h % 8 == 0;
   if (shard_world > 1 && !block_order) {  // no block order: a contiguous share of the path ids
     const uint64_t base = count / c->shard_world, rem = count % c->shard_world;
     first += c->shard_rank * base + std::min<uint64_t>(c->shard_rank, rem);
@@ -328,7 +337,8 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   // work order (see LaunchParams): pixel blocks with samples innermost, one
   // contiguous band of blocks per queue, when the launch covers whole samples
   const uint64_t P = L.tile_px;
-  const bool aligned = P && first % P == 0 && count % P == 0 && count > 0;
+  // (at most 2^20 samples: cvr_walk.h unit_to_path's pixel-of-unit division)
+  const bool aligned = P && first % P == 0 && count % P == 0 && count > 0 && count / P <= (1ull << 20);
   L.blk_off = 0;
   L.blk_stride = 1;
   if (c->order && aligned && c->tile_w % 8 == 0 && c->tile_h % 8 == 0) {
@@ -592,23 +602,35 @@ int mk_reference_render(cvr_ctx* c, const cvr::LaunchParams& L) {
 // them once the head has passed the last path) and compacts the survivors;
 // the host reads n_active and the head back, one sync per iteration as the
 // reference.  The RNG states stay with the threads (cvr_kernels.hip
-// k_smk_extend).  Temporary buffers per call: 2 x 3 float4 + 2 flags per slot,
-// 24 bytes of RNG state per thread.
+// k_smk_extend).  Buffers: 2 x 3 float4 + 2 flags per slot, 24 bytes of RNG
+// state per thread and two counters, carved from one allocation that stays
+// with the context (grown only when the grid grows).  Like the reference's
+// host loop, a call blocks the host until the render has ended.
 int smk_thread_render(cvr_ctx* c, const cvr::LaunchParams& L, uint32_t grid) {
   if (L.path_count == 0) return CVR_OK;
   const size_t n = (size_t)grid * 256u;
   const cvr::MediumParams m = launch_medium(c);
-  float4* slots = nullptr;
-  uint8_t* act = nullptr;
-  uint4* st0 = nullptr;
-  uint2* st1 = nullptr;
-  uint32_t* ctl = nullptr;
-  HIP_TRY(c, hipMalloc(&slots, 6 * n * sizeof(float4)));
-  hipError_t e = hipMalloc(&act, 2 * n);
-  if (e == hipSuccess) e = hipMalloc(&st0, n * sizeof(uint4));
-  if (e == hipSuccess) e = hipMalloc(&st1, n * sizeof(uint2));
-  if (e == hipSuccess) e = hipMalloc(&ctl, 2 * sizeof(uint32_t));
-  if (e == hipSuccess) e = hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), c->stream);  // d_n_active = head = 0
+  if (c->smk_n < n) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->d_smk) (void)hipFree(c->d_smk);
+    c->d_smk = nullptr;
+    c->smk_n = 0;
+    // float4 slots | uint4 states | uint2 states | flags | counters (every part 16-byte aligned)
+    const size_t bytes = 6 * n * sizeof(float4) + n * sizeof(uint4) + n * sizeof(uint2) + ((2 * n + 15) & ~(size_t)15) + 16;
+    HIP_TRY(c, hipMalloc(&c->d_smk, bytes));
+    c->smk_n = n;
+  }
+  unsigned char* p = c->d_smk;
+  float4* slots = reinterpret_cast<float4*>(p);
+  p += 6 * n * sizeof(float4);
+  uint4* st0 = reinterpret_cast<uint4*>(p);
+  p += n * sizeof(uint4);
+  uint2* st1 = reinterpret_cast<uint2*>(p);
+  p += n * sizeof(uint2);
+  uint8_t* act = p;
+  p += (2 * n + 15) & ~(size_t)15;
+  uint32_t* ctl = reinterpret_cast<uint32_t*>(p);
+  hipError_t e = hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), c->stream);  // d_n_active = head = 0
   cvr::SmkSlots buf[2] = {{slots, slots + n, slots + 2 * n, act}, {slots + 3 * n, slots + 4 * n, slots + 5 * n, act + n}};
   int cur = 0;  // the buffer d_regenerate writes and the next d_extend reads
   uint32_t h[2] = {(uint32_t)n, 0u};
@@ -627,11 +649,6 @@ int smk_thread_render(cvr_ctx* c, const cvr::LaunchParams& L, uint32_t grid) {
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   }
   c->last_iterations = (uint32_t)it;
-  (void)hipFree(slots);
-  if (act) (void)hipFree(act);
-  if (st0) (void)hipFree(st0);
-  if (st1) (void)hipFree(st1);
-  if (ctl) (void)hipFree(ctl);
   if (r) return r;
   if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "thread-bound streamingMK: %s", hipGetErrorString(e));
   return CVR_OK;
@@ -707,6 +724,7 @@ int cvr_destroy(cvr_ctx* c) {
   if (c->d_out_owned) (void)hipFree(c->d_out_owned);
   if (c->d_work) (void)hipFree(c->d_work);
   if (c->d_pool_T) (void)hipFree(c->d_pool_T);
+  if (c->d_smk) (void)hipFree(c->d_smk);
   if (c->d_block_perm) (void)hipFree(c->d_block_perm);
   if (c->d_zperm) (void)hipFree(c->d_zperm);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
@@ -1125,7 +1143,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->grid_override = (uint32_t)v;
       return CVR_OK;
     case CVR_OPT_SCHEDULER:
-      if (v < 0 || v > 3) return set_err(&c->err, CVR_ERR_INVALID, "scheduler must be 0..3");
+      if (v < 0 || v > kSchedPerItem) return set_err(&c->err, CVR_ERR_INVALID, "scheduler must be 0..4");
       c->scheduler = (int)v;
       return CVR_OK;
     case CVR_OPT_POOL:
@@ -1336,12 +1354,12 @@ int cvr_launch_render(cvr_ctx* c) {
       const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->cu_count * 2u;
       HIP_TRY(c, cvr::launch_stream_thread(launch_medium(c), L, c->kernel == CVR_KERNEL_SORTING_SK, grid, c->stream));
     }
-  } else if (c->kernel == CVR_KERNEL_NAIVE_SK) {
-    HIP_TRY(c, cvr::launch_naive(launch_medium(c), L, eps, c->stream));
   } else if (c->kernel == CVR_KERNEL_NAIVE_MK && c->mk_compaction) {
     if ((r = mk_reference_render(c, L))) return r;
   } else if (c->kernel == CVR_KERNEL_NAIVE_MK) {
     HIP_TRY(c, cvr::launch_naive_mk(launch_medium(c), L, c->stream));
+  } else if (scheduler_for(c) == kSchedPerItem) {
+    HIP_TRY(c, cvr::launch_naive(launch_medium(c), L, eps, c->stream));
   } else if (scheduler_for(c) == 0) {
     const uint32_t grid = c->grid_override ? c->grid_override : (uint32_t)c->persistent_grid;
     HIP_TRY(c, cvr::launch_persistent(launch_medium(c), L, eps, c->waves, grid, c->stream));
@@ -1494,7 +1512,7 @@ int cvr_trace_launch(cvr_ctx* c, cvr_path_record* out, uint64_t n_out) {
   int r = check_ready(c);
   if (r) return r;
   if ((r = do_init(c))) return r;
-  if (scheduler_for(c) != 3 || c->rng_binding || c->kernel == CVR_KERNEL_NAIVE_SK || c->kernel == CVR_KERNEL_NAIVE_MK)
+  if (scheduler_for(c) != 3 || c->rng_binding || c->kernel == CVR_KERNEL_NAIVE_MK)
     return set_err(&c->err, CVR_ERR_UNSUPPORTED, "cvr_trace_launch traces the wave-pool scheduler only");
   uint64_t first, count;
   compute_range(c, &first, &count);
@@ -1582,7 +1600,7 @@ int cvr_render_tiles(cvr_ctx* c, const cvr_render_desc* d, uint32_t first_tile, 
     // clear, launch, Scale + copy and seed advance as the loop below)
     if ((r = cvr_set_offset(c, 0, 0))) return r;
     if ((r = ensure_output(c))) return r;
-    return cvr_render_frame(c, host_image, 1, stats);
+    return cvr_render_frame(c, host_image, (size_t)W * H * 4u, 1, stats);
   }
   float4* dimg = static_cast<float4*>(device_image);
   float4* tmp_img = nullptr;
@@ -1644,6 +1662,66 @@ done:
     (void)hipFree(tmp_img);
   }
   return r;
+}
+
+// One device's share of a multi-device render (cvr --devices):
+// its tiles of the tile loop (tile k -> device k mod N, CudaVolPath.cpp:249-280
+// split over devices) or its block shard of the one tile, normalised and stored
+// by a kernel straight into the shared pinned host image at their places.  The
+// shares are pixel-disjoint, so N of these calls (one host thread per device)
+// leave cvr_render_image's image in the one host buffer: no reduction.
+int cvr_render_share_to_host(cvr_ctx* c, const cvr_render_desc* d, uint32_t first_tile, uint32_t tile_stride,
+                             float* host_image, size_t host_floats, cvr_stats* stats) {
+  if (!c || !d || !host_image) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
+  if (tile_stride == 0) return set_err(&c->err, CVR_ERR_INVALID, "tile stride 0");
+  const uint32_t W = d->resolution[0], H = d->resolution[1];
+  if (host_floats < (size_t)W * H * 4u)
+    return set_err(&c->err, CVR_ERR_INVALID, "host image holds %zu floats, the %ux%u image needs %zu", host_floats, W,
+                   H, (size_t)W * H * 4u);
+  if ((uintptr_t)host_image & 15u) return set_err(&c->err, CVR_ERR_INVALID, "host image must be 16-byte aligned");
+  int r = ensure_device(c);
+  if (r) return r;
+  void* dhost = nullptr;  // the host image's device address (pinned / registered memory)
+  hipError_t e = hipHostGetDevicePointer(&dhost, host_image, 0);
+  if (e != hipSuccess || !dhost) {
+    (void)hipGetLastError();
+    return set_err(&c->err, CVR_ERR_INVALID, "host image is not pinned or registered (cvr_host_alloc)");
+  }
+  const uint32_t ntiles = d->n_tiles[0] * d->n_tiles[1];
+  if (ntiles != 1 || c->shard_world == 1) {
+    // tiles k = first_tile, first_tile + stride, ...: each tile's pixels only (k_tile_to_image
+    // into the mapped host image), each tile with its sequential-loop seed
+    if (ntiles != 1 && c->shard_world != 1)
+      return set_err(&c->err, CVR_ERR_INVALID, "a tile share and a block shard at once");
+    return cvr_render_tiles(c, d, first_tile, tile_stride, dhost, nullptr, stats);
+  }
+  // one tile, this context's block shard: launch, then its 8x8 blocks into the host image
+  if (first_tile != 0) return set_err(&c->err, CVR_ERR_INVALID, "one tile: the share is the block shard");
+  if (W % 8 || H % 8) return set_err(&c->err, CVR_ERR_INVALID, "block shards need sides that are multiples of 8");
+  if ((r = cvr_set_resolution(c, W, H)) || (r = cvr_set_iterations(c, d->iterations)) || (r = cvr_set_offset(c, 0, 0)))
+    return r;
+  if ((r = check_ready(c)) || (r = ensure_output(c))) return r;
+  if ((r = cvr_clear_output(c)) || (r = cvr_launch_render(c))) return r;
+  e = cvr::launch_blocks_to_host(reinterpret_cast<const float*>(c->d_out), static_cast<float*>(dhost), W, H,
+                                 c->shard_rank, c->shard_world, (float)d->iterations, c->stream);
+  if (e != hipSuccess) return set_err(&c->err, CVR_ERR_HIP, "blocks to host: %s", hipGetErrorString(e));
+  cvr_stats s{};
+  if ((r = cvr_get_stats(c, &s))) return r;  // synchronises: the blocks are in the host image
+  if (stats) *stats = s;
+  return cvr_reset(c);  // prepareForNextIterations
+}
+
+int cvr_host_alloc(size_t bytes, void** out) {
+  if (!out) return set_err(nullptr, CVR_ERR_INVALID, "NULL argument");
+  *out = nullptr;
+  const hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable);
+  if (e != hipSuccess) return set_err(nullptr, CVR_ERR_HIP, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  return CVR_OK;
+}
+
+int cvr_host_free(void* p) {
+  if (p && hipHostFree(p) != hipSuccess) return set_err(nullptr, CVR_ERR_HIP, "hipHostFree failed");
+  return CVR_OK;
 }
 
 // The launcher settings a helper context of cvr_render_frame takes from its
@@ -1768,10 +1846,13 @@ int cvr_frame_flush_info(const cvr_ctx* c, uint32_t* blocks, uint32_t* fallbacks
   return CVR_OK;
 }
 
-int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* stats) {
+int cvr_render_frame(cvr_ctx* c, float* host_image, size_t host_floats, uint32_t parts, cvr_stats* stats) {
   if (!c || !host_image) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   int r = check_ready(c);
   if (r) return r;
+  if (host_floats < (size_t)c->tile_w * c->tile_h * 4u)
+    return set_err(&c->err, CVR_ERR_INVALID, "host image holds %zu floats, the %ux%u tile needs %zu", host_floats,
+                   c->tile_w, c->tile_h, (size_t)c->tile_w * c->tile_h * 4u);
   if (!c->d_out) return set_err(&c->err, CVR_ERR_STATE, "no output buffer");
   if ((r = do_init(c))) return r;
   const uint32_t W = c->tile_w, H = c->tile_h;
@@ -1781,7 +1862,7 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, uint32_t parts, cvr_stats* s
   compute_range(c, &first, &count);
   cvr::LaunchParams L0{};
   fill_launch(c, L0, first, count);
-  const bool queued = c->kernel != CVR_KERNEL_NAIVE_SK && c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 &&
+  const bool queued = c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 && scheduler_for(c) != kSchedPerItem &&
                       c->rng_binding == 0;
   const uint32_t brows = (L0.order == 1 && queued && c->shard_world == 1) ? H / 8u : 0u;
   if (parts == 0) parts = 1;

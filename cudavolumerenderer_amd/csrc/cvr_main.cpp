@@ -7,18 +7,24 @@
 //       [--iterations|-i N] [--resolution|-r W [H]] [--number-of-tiles X [Y]]
 //       [--trials N] [--output|-o NAME] [--interactive BOOL]
 //       [--use-unified-memory BOOL]
-//   extensions: --synthetic bucky|manix|hetvol|cloud, --device N, --seed S
+//   extensions: --synthetic bucky|manix|hetvol|cloud, --device N, --seed S,
+//   --devices N|d0,d1,... (one context per device, each on its own host
+//   thread: tile k -> device k mod N for --number-of-tiles, else 8x8-block
+//   shards of the one tile; every device stores its pixels straight into one
+//   pinned host image), --pfm (also write the float image as <output>.pfm)
 //
 // Differences from the reference, on purpose: the timer is wall clock (the
 // reference uses clock(), i.e. CPU time, Main.cpp:51-77); main does not wait
 // for Enter; --interactive true has no GL viewer here (out of scope, SURVEY
 // §2.1) and falls back to the headless path with a notice.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cvr.h"
@@ -28,6 +34,8 @@ namespace {
 struct Options {
   std::string scene_file, scene_type = "Auto", algorithm = "cudaVolPath", kernel = "regenerationSK";
   std::string output, synthetic, rng_binding = "path", world_to_aabb = "reference", mk_compaction = "fixed";
+  std::string devices;  // --devices: a count or a comma list of device ids
+  bool pfm = false;
   std::vector<float> default_albedo;
   bool interactive = true, unified = false;
   unsigned trials = 1, iterations = 20, device = 0, seed = 0;
@@ -55,6 +63,10 @@ void usage() {
       "Extensions:\n"
       "  --synthetic bucky|manix|hetvol|cloud  use a built-in proxy scene\n"
       "  --device N, --seed S\n"
+      "  --devices N|d0,d1,...              render on several devices at once (one context and host\n"
+      "                                     thread each; ids may repeat): tile k -> device k mod N\n"
+      "                                     with --number-of-tiles, else 8x8-block shards of the image\n"
+      "  --pfm                              also write the float image as <output>.pfm\n"
       "  --rng-binding path|thread (=path)  regenerationSK: thread = the reference's Rng(seed + tid)\n"
       "                                     per persistent thread (non-deterministic, SURVEY Q2)\n"
       "  --default-albedo r g b             VDB files without an albedo grid load with this albedo\n"
@@ -99,6 +111,8 @@ int parse(int argc, char** argv, Options& o) {
     else if (a == "-r" || a == "--resolution") multi(o.resolution);
     else if (a == "--synthetic") o.synthetic = need("synthetic");
     else if (a == "--device") o.device = (unsigned)strtoul(need("device").c_str(), nullptr, 10);
+    else if (a == "--devices") o.devices = need("devices");
+    else if (a == "--pfm") o.pfm = true;
     else if (a == "--rng-binding") o.rng_binding = need("rng-binding");
     else if (a == "--seed") o.seed = (unsigned)strtoul(need("seed").c_str(), nullptr, 10);
     else if (a == "--world-to-aabb") o.world_to_aabb = need("world-to-aabb");
@@ -122,6 +136,40 @@ int parse(int argc, char** argv, Options& o) {
   if (o.tiles.size() == 1) o.tiles.push_back(o.tiles[0]);
   if (o.resolution.size() == 1) o.resolution.push_back(o.resolution[0]);
   return 0;
+}
+
+// --devices: "N" (devices first..first+N-1) or "d0,d1,..." (ids may repeat: several
+// contexts on one device, each with its own stream and work queues)
+std::vector<int> parse_devices(const std::string& v, unsigned first) {
+  std::vector<int> d;
+  if (v.empty()) return {(int)first};
+  if (v.find(',') == std::string::npos) {
+    const unsigned n = (unsigned)strtoul(v.c_str(), nullptr, 10);
+    for (unsigned k = 0; k < n; ++k) d.push_back((int)(first + k));
+    return d;
+  }
+  size_t p = 0;
+  while (p <= v.size()) {
+    const size_t q = std::min(v.find(',', p), v.size());
+    d.push_back((int)strtoul(v.substr(p, q - p).c_str(), nullptr, 10));
+    p = q + 1;
+  }
+  return d;
+}
+
+// Portable float map (little-endian RGB, rows bottom to top): the image as floats,
+// for comparisons the RGBE .hdr cannot hold.
+int write_pfm(const std::string& path, const float* rgba, unsigned w, unsigned h) {
+  FILE* f = fopen(path.c_str(), "wb");
+  if (!f) return 1;
+  fprintf(f, "PF\n%u %u\n-1.0\n", w, h);
+  std::vector<float> row((size_t)w * 3);
+  for (unsigned y = h; y-- > 0;) {
+    for (unsigned x = 0; x < w; ++x)
+      for (int c = 0; c < 3; ++c) row[(size_t)x * 3 + c] = rgba[((size_t)y * w + x) * 4 + c];
+    fwrite(row.data(), sizeof(float), row.size(), f);
+  }
+  return fclose(f) != 0;
 }
 
 int scene_type_id(const std::string& t) {
@@ -202,54 +250,125 @@ int main(int argc, char** argv) {
   std::vector<float> image((size_t)W * H * 4, 0.0f);
   std::vector<double> times;
   double mean = 0;
+  if (o.rng_binding != "path" && o.rng_binding != "thread") {
+    fprintf(stderr, "[ConfigParser] Error: --rng-binding must be path or thread\n");
+    return 2;
+  }
+  if (o.world_to_aabb != "reference" && o.world_to_aabb != "fixed") {
+    fprintf(stderr, "[ConfigParser] Error: --world-to-aabb must be reference or fixed\n");
+    return 2;
+  }
+  if (o.mk_compaction != "fixed" && o.mk_compaction != "reference") {
+    fprintf(stderr, "[ConfigParser] Error: --mk-compaction must be fixed or reference\n");
+    return 2;
+  }
+  // One context: its options, the medium (its own upload, or `share`'s device copy when
+  // another context on the same device already holds it), the camera.
+  auto make_ctx = [&](int device, cvr_ctx* share) -> cvr_ctx* {
+    cvr_ctx* ctx = nullptr;
+    if (cvr_create(device, kernel, &ctx) != CVR_OK) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(nullptr));
+      return nullptr;
+    }
+    int rc = cvr_set_seed(ctx, o.seed);
+    if (!rc && o.rng_binding == "thread") rc = cvr_set_option(ctx, CVR_OPT_RNG_BINDING, 1);
+    if (!rc && o.world_to_aabb == "fixed") rc = cvr_set_option(ctx, CVR_OPT_WORLD_TO_AABB, 1);
+    if (!rc && o.mk_compaction == "reference") rc = cvr_set_option(ctx, CVR_OPT_MK_COMPACTION, 1);
+    if (!rc && share) {
+      rc = cvr_share_medium(ctx, share);
+    } else if (!rc) {
+      if (!sparse && (rc = cvr_set_medium(ctx, &md)) == CVR_ERR_UNSUPPORTED) {
+        printf("[Scene] dense grid rejected (%s); using the sparse leaf upload\n", cvr_last_error(ctx));
+        if ((rc = cvr_scene_sparse_medium(scene, &sd)) == CVR_OK) sparse = true;
+      }
+      if (!rc && sparse) rc = cvr_set_medium_sparse(ctx, &sd);
+    }
+    if (!rc) rc = cvr_set_camera(ctx, inv_view, r2v, full_res);
+    if (!rc) rc = cvr_init(ctx);
+    if (rc) {
+      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
+      cvr_destroy(ctx);
+      return nullptr;
+    }
+    return ctx;
+  };
+  const std::vector<int> devs = parse_devices(o.devices, o.device);
+  if (devs.empty()) {
+    fprintf(stderr, "[ConfigParser] Error: --devices needs a count or a list of device ids\n");
+    return 2;
+  }
+  const unsigned ntiles = o.tiles[0] * o.tiles[1];
+  size_t n_dev = devs.size();
+  const bool tile_mode = ntiles > 1;
+  if (n_dev > 1 && !tile_mode && (W % 8 || H % 8)) {
+    printf("[Devices] one tile of %ux%u: block shards need sides that are multiples of 8; rendering on device %d\n", W,
+           H, devs[0]);
+    n_dev = 1;
+  }
+  if (n_dev > 1) {
+    printf("[Devices] %zu contexts on devices", n_dev);
+    for (int dv : devs) printf(" %d", dv);
+    printf(": %s\n", tile_mode ? "tile k -> context k mod N" : "8x8-block shards of the image");
+  }
+  float* himg = nullptr;  // the shared pinned host image (multi-device)
+  if (n_dev > 1 && cvr_host_alloc((size_t)W * H * 4 * sizeof(float), reinterpret_cast<void**>(&himg)) != CVR_OK) {
+    fprintf(stderr, "Error: %s\n", cvr_last_error(nullptr));
+    return 1;
+  }
+  cvr_render_desc d = {{W, H}, {o.tiles[0], o.tiles[1]}, o.iterations};
   for (unsigned t = 0; t < o.trials; ++t) {
     printf("---------------------------------------------------------------trial : %u \n", t);
-    cvr_ctx* ctx = nullptr;
-    if ((r = cvr_create((int)o.device, kernel, &ctx)) != CVR_OK) {
-      fprintf(stderr, "Error: %s\n", cvr_last_error(nullptr));
-      return 1;
+    std::vector<cvr_ctx*> ctxs;
+    for (size_t k = 0; k < n_dev; ++k) {
+      cvr_ctx* share = nullptr;  // the first context on this device holds its medium
+      for (size_t j = 0; j < k; ++j)
+        if (devs[j] == devs[k]) {
+          share = ctxs[j];
+          break;
+        }
+      cvr_ctx* c = make_ctx(devs[k], share);
+      if (!c) return 1;
+      if (n_dev > 1 && !tile_mode && (r = cvr_set_block_shard(c, (uint32_t)k, (uint32_t)n_dev)) != CVR_OK) {
+        fprintf(stderr, "Error: %s\n", cvr_last_error(c));
+        return 1;
+      }
+      ctxs.push_back(c);
     }
-    cvr_set_seed(ctx, o.seed);
-    if (o.rng_binding != "path" && o.rng_binding != "thread") {
-      fprintf(stderr, "[ConfigParser] Error: --rng-binding must be path or thread\n");
-      return 2;
-    }
-    if (o.rng_binding == "thread" && (r = cvr_set_option(ctx, CVR_OPT_RNG_BINDING, 1)) != CVR_OK) {
-      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
-      return 1;
-    }
-    if (o.world_to_aabb != "reference" && o.world_to_aabb != "fixed") {
-      fprintf(stderr, "[ConfigParser] Error: --world-to-aabb must be reference or fixed\n");
-      return 2;
-    }
-    if (o.mk_compaction != "fixed" && o.mk_compaction != "reference") {
-      fprintf(stderr, "[ConfigParser] Error: --mk-compaction must be fixed or reference\n");
-      return 2;
-    }
-    if ((o.world_to_aabb == "fixed" && (r = cvr_set_option(ctx, CVR_OPT_WORLD_TO_AABB, 1)) != CVR_OK) ||
-        (o.mk_compaction == "reference" && (r = cvr_set_option(ctx, CVR_OPT_MK_COMPACTION, 1)) != CVR_OK)) {
-      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
-      return 1;
-    }
-    if (!sparse && (r = cvr_set_medium(ctx, &md)) == CVR_ERR_UNSUPPORTED) {
-      printf("[Scene] dense grid rejected (%s); using the sparse leaf upload\n", cvr_last_error(ctx));
-      if ((r = cvr_scene_sparse_medium(scene, &sd)) != CVR_OK) return 1;
-      sparse = true;
-    }
-    if (sparse) r = cvr_set_medium_sparse(ctx, &sd);
-    if (r || (r = cvr_set_camera(ctx, inv_view, r2v, full_res)) || (r = cvr_init(ctx))) {
-      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
-      return 1;
-    }
-    cvr_render_desc d = {{W, H}, {o.tiles[0], o.tiles[1]}, o.iterations};
-    cvr_stats st;
+    cvr_stats st{};
     const auto t0 = std::chrono::steady_clock::now();
-    r = cvr_render_image(ctx, &d, nullptr, image.data(), &st);
-    const auto t1 = std::chrono::steady_clock::now();
-    if (r != CVR_OK) {
-      fprintf(stderr, "Error: %s\n", cvr_last_error(ctx));
-      return 1;
+    if (n_dev == 1) {
+      r = cvr_render_image(ctxs[0], &d, nullptr, image.data(), &st);
+      if (r != CVR_OK) {
+        fprintf(stderr, "Error: %s\n", cvr_last_error(ctxs[0]));
+        return 1;
+      }
+    } else {
+      std::fill(himg, himg + (size_t)W * H * 4, 0.0f);  // pixels no tile covers stay 0 (Q1)
+      std::vector<cvr_stats> sts(n_dev);
+      std::vector<int> rcs(n_dev, CVR_OK);
+      std::vector<std::string> errs(n_dev);
+      std::vector<std::thread> th;
+      for (size_t k = 0; k < n_dev; ++k)
+        th.emplace_back([&, k] {
+          rcs[k] = cvr_render_share_to_host(ctxs[k], &d, tile_mode ? (uint32_t)k : 0u, tile_mode ? (uint32_t)n_dev : 1u,
+                                            himg, (size_t)W * H * 4, &sts[k]);
+          if (rcs[k] != CVR_OK) errs[k] = cvr_last_error(ctxs[k]);
+        });
+      for (auto& x : th) x.join();
+      for (size_t k = 0; k < n_dev; ++k) {
+        if (rcs[k] != CVR_OK) {
+          fprintf(stderr, "Error (context %zu, device %d): %s\n", k, devs[k], errs[k].c_str());
+          return 1;
+        }
+        st.paths += sts[k].paths;
+        st.segments += sts[k].segments;
+        st.steps += sts[k].steps;
+        st.escaped += sts[k].escaped;
+        st.kernel_ms = std::max(st.kernel_ms, sts[k].kernel_ms);
+      }
     }
+    const auto t1 = std::chrono::steady_clock::now();
+    if (n_dev > 1) std::copy(himg, himg + (size_t)W * H * 4, image.begin());
     const double sec = std::chrono::duration<double>(t1 - t0).count();
     printf("rendering time      : %.2f sec \n", sec);
     printf("total traced rays %llu (woodcock steps %llu)\n", (unsigned long long)st.segments,
@@ -258,9 +377,14 @@ int main(int argc, char** argv) {
       times.push_back(sec);
       mean += sec;
     }
-    cvr_destroy(ctx);
+    for (size_t k = n_dev; k-- > 0;) cvr_destroy(ctxs[k]);  // sharers before the medium's owner
     cvr_write_hdr((o.output + ".hdr").c_str(), image.data(), W, H);
+    if (o.pfm && write_pfm(o.output + ".pfm", image.data(), W, H)) {
+      fprintf(stderr, "Error: could not write %s.pfm\n", o.output.c_str());
+      return 1;
+    }
   }
+  if (himg) cvr_host_free(himg);
   if (o.trials > 1) {
     mean /= (double)times.size();
     double var = 0;

@@ -74,13 +74,18 @@ CVR_DEV void rng_init(Rng& s, int32_t seed) {
   s.v3 = 88675123u ^ t1;
   s.v4 = 5783321u + t0;
 }
+// Three-input xor as gfx950's v_bitop3_b32 (truth table 0x96 = a ^ b ^ c):
+// hipcc 7.2 does not form it from a ^ b ^ c (it emits two v_xor_b32).
+CVR_DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 CVR_DEV uint32_t rng_next(Rng& s) {
   const uint32_t t = s.v0 ^ (s.v0 >> 2);
   s.v0 = s.v1;
   s.v1 = s.v2;
   s.v2 = s.v3;
   s.v3 = s.v4;
-  s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+  // (v4 ^ (v4 << 4)) ^ (t ^ (t << 1)): xor is associative, so the same word
+  // with one v_bitop3 and one v_xor instead of three v_xor (6 VALU per word, was 7)
+  s.v4 = xor3(s.v4, s.v4 << 4, t) ^ (t << 1);
   s.d += 362437u;
   return s.v4 + s.d;
 }
@@ -88,7 +93,7 @@ CVR_DEV uint32_t rng_next(Rng& s) {
 // new word is n = (v4 ^ (v4 << 4)) ^ (u ^ (u << 1)) with u = v0 ^ (v0 >> 2);
 // both xorshifts are invertible by prefix xors.
 CVR_DEV void rng_undo(Rng& s) {
-  uint32_t u = s.v4 ^ s.v3 ^ (s.v3 << 4);  // = u ^ (u << 1)
+  uint32_t u = xor3(s.v4, s.v3, s.v3 << 4);  // = u ^ (u << 1)
   u ^= u << 1;
   u ^= u << 2;
   u ^= u << 4;
@@ -277,6 +282,17 @@ CVR_DEV uint32_t queue_units(const LaunchParams& L, uint32_t q) {
   if (L.order == 0) return q == 0 ? L.path_count : 0u;
   return (queue_blocks_begin(L, q + 1) - queue_blocks_begin(L, q)) * 64u * L.samples;
 }
+// Within a block the units run pixel by pixel with the pixel's samples
+// innermost (round 5, CVR_UNIT_SAMPLE_INNER; before: the 64 pixels of sample
+// 0, then of sample 1, ...), so the paths a wave holds at once belong to a few
+// pixels, and the escapes of one event batch mostly share pixels, whose
+// framebuffer adds the batch then combines (splat_wave).  The pixel of unit
+// rem of a block is rem / samples = (rem << 6) / (64 samples), one fastdiv by
+// the block divisor (exact while 64 * 64 * samples <= 2^32: the host keeps
+// launches with more than 2^20 samples in path-id order).
+#ifndef CVR_UNIT_SAMPLE_INNER
+#define CVR_UNIT_SAMPLE_INNER 1
+#endif
 CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.order == 0) return L.path_first + u;
   const uint32_t per_block = 64u * L.samples;
@@ -285,7 +301,11 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.block_perm) bl = gmem(L.block_perm)[bl];
   const uint32_t b = L.blk_off + __umul24(bl, L.blk_stride);
   const uint32_t rem = u - bq * per_block;
+#if CVR_UNIT_SAMPLE_INNER
+  const uint32_t lane = fastdiv(rem << 6, L.div_block), s = rem - lane * L.samples;
+#else
   const uint32_t s = rem >> 6, lane = rem & 63u;
+#endif
   const uint32_t by = fastdiv(b, L.div_blocks_x);
   const uint32_t px = (b - by * L.blocks_x) * 8u + (lane & 7u), py = by * 8u + (lane >> 3);
   return L.path_first + s * L.tile_px + py * L.tile_w + px;

@@ -35,6 +35,11 @@
 // Tentative points per lane per Woodcock group (the lookahead below).  The
 // track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
 constexpr int kLook = 2;
+// The track loop runs CVR_WPOOL_UNROLL / kLook groups: a variant build with
+// UNROLL < kLook would run none (tracking lanes never step: the launch never
+// ends), one with a remainder would silently drop the remainder's steps.
+static_assert(CVR_WPOOL_UNROLL >= kLook && CVR_WPOOL_UNROLL % kLook == 0,
+              "CVR_WPOOL_UNROLL must be a positive multiple of kLook");
 // Wave priorities (s_setprio): the track loop above the event code, so a
 // stepping wave issues its brick-bound and cell loads ahead of the
 // VALU-dense event batches of the other waves on its SIMD (C2: -0.7%).
@@ -172,6 +177,77 @@ __device__ __forceinline__ void load_track(const WavePool<kSlots>& S, uint32_t s
 }
 
 enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
+
+// The batch's escapes, combined per pixel before the framebuffer atomics
+// (atomicVectorAdd, Utilities.cuh:15-22, once per escape in the reference).
+// The framebuffer adds are performed at the memory side (the XCDs' L2s are not
+// coherent), up to three float adds and the w swap per escape; with the units'
+// samples innermost (unit_to_path) the escapes of one batch mostly share a few
+// pixels.  Each escaping lane finds its pixel's leader (the lowest lane with
+// that pixel: one ballot per distinct pixel), the others add their T into the
+// leader's freed slot in LDS (ds_add_f32; the path has ended, its slot goes to
+// the new-path stack and no later part of this batch touches it), and each
+// leader issues one splat of its pixel's sum.  Only the order of the fp32
+// additions changes, so the per-pixel bound of DESIGN.md §4 holds: a pixel's
+// n contributions are still summed once each, in some order.  With no pixel
+// escaped to twice the batch splats per lane as before.
+#ifndef CVR_WPOOL_SPLAT_COMBINE
+#define CVR_WPOOL_SPLAT_COMBINE 1
+#endif
+template <int kSlots>
+__device__ __forceinline__ void splat_wave(WavePool<kSlots>& S, const LaunchParams& L, const PathState& ps, bool esc,
+                                           uint32_t s, uint32_t lane) {
+#if defined(CVR_DIAG_NO_SPLAT)  // diagnostic timing builds only (wrong images): no framebuffer writes
+  (void)S; (void)L; (void)ps; (void)esc; (void)s; (void)lane;
+  return;
+#endif
+#if CVR_WPOOL_SPLAT_COMBINE
+  unsigned long long rest = __ballot(esc);
+  if (rest == 0ull) return;
+  uint32_t leader = lane;
+  bool multi = false;  // wave-uniform: some pixel gets two or more escapes
+  while (rest != 0ull) {
+    const uint32_t l0 = (uint32_t)__builtin_ctzll(rest);
+    const uint32_t id0 = __builtin_amdgcn_readlane(ps.image_id, l0);
+    const unsigned long long g = __ballot(esc && ps.image_id == id0);
+    if (esc && ps.image_id == id0) leader = l0;
+    multi |= (g & (g - 1ull)) != 0ull;
+    rest &= ~g;
+  }
+  if (!multi) {
+    if (esc) splat(L, ps);
+    return;
+  }
+  const uint32_t sl = (uint32_t)__shfl((int)s, (int)leader);  // the leader's slot
+  float* acc = reinterpret_cast<float*>(&S.a[sl]);
+  const bool lead = esc && leader == lane;
+  if (lead) {
+    acc[0] = ps.T.x;
+    acc[1] = ps.T.y;
+    acc[2] = ps.T.z;
+  }
+  // one wave: its LDS instructions are performed in order; the wait keeps the
+  // compiler from moving the adds above the leaders' stores
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (esc && !lead) {
+    __hip_atomic_fetch_add(acc + 0, ps.T.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(acc + 1, ps.T.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_fetch_add(acc + 2, ps.T.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (lead) {
+    PathState q{};
+    q.image_id = ps.image_id;
+    q.T = mk3(acc[0], acc[1], acc[2]);
+    splat(L, q);
+  }
+#else
+  (void)S;
+  (void)s;
+  (void)lane;
+  if (esc) splat(L, ps);
+#endif
+}
 
 // The wave's path cursor into the global work queues (as k_persistent).
 // Debug records (LaunchParams::rec): a path's final state when it ends, in
@@ -774,8 +850,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             ++nseg;
             seg_first = true;
             if (!aabb_intersect(me, ps.o, ps.d, is)) {
-              splat(L, ps);
-              escaped = true;
+              escaped = true;  // splat below (splat_wave)
               to_ln = true;
               if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
               if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
@@ -818,8 +893,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           ++nseg;
           seg_next = true;
           if (!aabb_intersect(me, ps.o, ps.d, is)) {
-            splat(L, ps);
-            escaped = true;
+            escaped = true;  // splat below (splat_wave)
             to_ln = true;
             if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
             if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
@@ -830,6 +904,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           }
         }
       }
+      // the batch's escapes (camera rays that miss the box, survivors leaving it), per pixel
+      splat_wave(S, L, ps, escaped, s, lane);
       // a path's segments are the increments of its nseg (each counted once, as
       // the reference's per-iteration RAYS_STATISTICS count)
       {

@@ -195,6 +195,16 @@ class HostImage:
         self._hip = hip
         rc = hip.hipHostRegister(ctypes.c_void_p(self.flat.data_ptr()), nbytes, 2)  # hipHostRegisterMapped
         if rc != 0:
+            # no barrier here (the other ranks may have registered and moved on): drop this rank's
+            # view and, on rank 0, the /dev/shm file, so that a failed run leaves no shared memory
+            self.flat = None
+            self._mm = None
+            del mm
+            if rank == 0:
+                try:
+                    os.unlink(self.path)
+                except OSError:
+                    pass
             raise RuntimeError(f"rank {rank}: hipHostRegister of the shared host image {self.path} failed "
                                f"(hipError {rc}); refusing to run with an unpinned image")
         self.pinned = self._registered = True

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CVR_ABI_VERSION 2
+#define CVR_ABI_VERSION 3  /* 3: cvr_render_frame takes the host buffer size */
 
 enum {
   CVR_OK = 0,
@@ -66,8 +66,14 @@ typedef enum {
   CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
   CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
   CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
-  CVR_OPT_SCHEDULER = 6,      /* regenerationSK: 0 single persistent kernel, 1 wavefront pair,
-                                 2 workgroup path pool in LDS, 3 wave-private path pool in LDS (default) */
+  CVR_OPT_SCHEDULER = 6,      /* how paths map onto threads, for every kernel id but naiveMK:
+                                 0 single persistent kernel, 1 wavefront pair (streamingMK's
+                                 multi-kernel structure), 2 workgroup path pool in LDS (streamingSK's
+                                 block streaming), 3 wave-private path pool in LDS (the default for
+                                 all of them; round 4 and before: naiveSK 4, streamingSK 2,
+                                 streamingMK 1), 4 one path per work-item (naiveSK's structure).
+                                 Scheduling only: results depend on the kernel id, not on the
+                                 scheduler. */
   CVR_OPT_POOL = 7,           /* wavefront ray-slot pool size (default 2^21) */
   CVR_OPT_TIMING = 8,         /* 1: time every wavefront kernel (track_ms / events_ms) */
   CVR_OPT_CELLS = 9           /* 1 (default): corner-replicated density cells (8x density bytes
@@ -99,8 +105,17 @@ typedef enum {
                                  paths (StreamingVolPTmk_kernel.cuh:26-253).  Thread-bound results
                                  depend on which thread takes which path: deterministic only for a
                                  one-wave (regenerationSK) or one-block (streaming/sorting/
-                                 streamingMK) launch, CVR_OPT_GRID 1. */
-  CVR_OPT_MORTON = 17,         /* pool scheduler (streamingSK): 1 sorts each track phase's paths by the
+                                 streamingMK) launch, CVR_OPT_GRID 1.  Reproduced quirk Q23
+                                 (streamingSK / sortingSK): the sort key of an inactive thread is
+                                 morton3D(1,1,1) = 2^30 - 1 (MortonSort.h:39-43), which an active
+                                 path whose origin lies within 1/1024 of box_max on all three axes
+                                 also gets; the stable tie-break on the thread index can then place
+                                 that path past n_active, where the next regeneration overwrites it
+                                 (dropped without a splat, not counted as truncated), as in the
+                                 reference's cub sort.  streamingMK with 1 blocks the host until the
+                                 render ends (one stream sync per iteration, as the reference's host
+                                 loop). */
+  CVR_OPT_MORTON = 17,         /* workgroup pool scheduler (CVR_OPT_SCHEDULER 2): 1 sorts each track phase's paths by the
                                  Morton code of their origin in the box (MortonSort.h:28-49,
                                  StreamingVolPTsk_kernel.cuh:188-216); default 0 (measured slower
                                  here).  Scheduling only: results are unchanged. */
@@ -318,8 +333,10 @@ int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats,
  * eight flusher waves store
  * each 8x8 block, normalised, as soon as all of its paths have ended, so the
  * image is complete when the kernel ends; if a flusher gives up (no block
- * finished for a second) the call copies the image the usual way instead. */
-int cvr_render_frame(cvr_ctx* ctx, float* host_image, uint32_t parts, cvr_stats* stats);
+ * finished for a second) the call copies the image the usual way instead.
+ * host_floats: the floats host_image holds; fewer than tile_w * tile_h * 4
+ * (cvr_get_resolution) is CVR_ERR_INVALID and nothing is rendered (ABI 3). */
+int cvr_render_frame(cvr_ctx* ctx, float* host_image, size_t host_floats, uint32_t parts, cvr_stats* stats);
 /* The last cvr_render_frame's in-launch output: blocks the flushers stored (0
  * if the call copied after the launch) and the number of calls so far that
  * fell back to the copy because a flusher gave up. */
@@ -376,6 +393,25 @@ int cvr_render_image(cvr_ctx* ctx, const cvr_render_desc* desc, void* device_ima
  * rendered tiles.  cvr_render_image == cvr_render_tiles(ctx, desc, 0, 1, ...). */
 int cvr_render_tiles(cvr_ctx* ctx, const cvr_render_desc* desc, uint32_t first_tile, uint32_t tile_stride,
                      void* device_image, float* host_image, cvr_stats* stats);
+/* Extension (multi-device renderer; the CLI's --devices): one
+ * device's share of a render, stored normalised by a kernel straight into the
+ * full pinned host image (cvr_host_alloc, or registered memory; width *
+ * height * 4 floats, host_floats checked) at its places, nothing else written:
+ *  - more than one tile (desc->n_tiles): tiles first_tile, first_tile +
+ *    tile_stride, ... of the tile loop (tile k -> device k mod N,
+ *    CudaVolPath.cpp:249-280), each with its sequential-loop seed;
+ *  - one tile: the context's block shard (cvr_set_block_shard; sides multiples
+ *    of 8; first_tile must be 0).
+ * Disjoint shares from N contexts (one host thread each, any devices) leave
+ * cvr_render_image's image in the one buffer, with no reduction.  Synchronous;
+ * stats cover this share. */
+int cvr_render_share_to_host(cvr_ctx* ctx, const cvr_render_desc* desc, uint32_t first_tile, uint32_t tile_stride,
+                             float* host_image, size_t host_floats, cvr_stats* stats);
+/* Pinned, device-mapped host memory for cvr_render_share_to_host /
+ * cvr_render_frame's in-launch output (hipHostMalloc, mapped + portable: every
+ * device can store into it), and its release. */
+int cvr_host_alloc(size_t bytes, void** out);
+int cvr_host_free(void* p);
 
 /* ---- camera / tiling helpers ------------------------------------------ */
 /* Default Camera (Camera.h:25-71, MITSUBA_COMPARABLE) after

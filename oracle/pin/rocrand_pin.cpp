@@ -7,7 +7,7 @@
 // float mapping.  This program loads a state (v0..v4, d) given on the command
 // line into rocRAND's engine and prints its next() outputs, so that the
 // oracle's state-transition function can be checked against an independent
-// implementation (tests/test_oracle_pins.py).
+// implementation (tests/test_oracle_cpu.py).
 //
 //   rocrand_pin v0 v1 v2 v3 v4 d n   -> n decimal u32 values, one per line
 #include <rocrand/rocrand_xorwow.h>

@@ -1,0 +1,102 @@
+"""The CLI's multi-device render (cvr --devices, SURVEY §8(e) from the drop-in
+surface): one context per device, each on its own host thread, storing its
+pixel-disjoint share (tile k -> context k mod N with --number-of-tiles, else
+8x8-block shards of the one tile) straight into one pinned host image through
+cvr_render_share_to_host, with no reduction and no torch.
+
+The leased box has one GPU, so the contexts share device 0 (`--devices
+0,0,0`): each still has its own stream, work queues and wave-pool scratch, and
+the shares are exactly the ones N devices would render.  The image (written as
+a float .pfm) must equal cvr_render_image's single-context render within the
+summation-order bound."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from parity_util import assert_pixels_close
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(ROOT, "cudavolumerenderer_amd", "cvr")
+
+
+def read_pfm(path):
+    with open(path, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        scale = float(f.readline())
+        assert scale < 0  # little-endian
+        a = np.frombuffer(f.read(), dtype="<f4").reshape(h, w, 3)
+    return a[::-1]  # rows bottom to top
+
+
+def run_cli(tmp_path, name, *args):
+    out = str(tmp_path / name)
+    r = subprocess.run([CLI, "--interactive", "0", "--pfm", "-o", out, *args], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return read_pfm(out + ".pfm"), r.stdout
+
+
+def reference_image(cvr, scene_name, W, H, tiles, iters, kernel="regenerationSK"):
+    scene = cvr.Scene.synthetic(scene_name)
+    c = cvr.Context(0, kernel)
+    c.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(W, H)
+    c.set_camera(iv, r2v, (W, H))
+    c.init()
+    img, _ = c.render_image(W, H, tiles, iters)
+    c.close()
+    return img[..., :3]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0"])
+def test_cli_block_shards_equal_one_context(cvr, tmp_path, devices):
+    W, H, iters = 256, 192, 4
+    img, out = run_cli(tmp_path, "blk", "--synthetic", "manix", "-r", str(W), str(H), "-i", str(iters),
+                       "--devices", devices)
+    n = len(devices.split(","))
+    assert f"[Devices] {n} contexts" in out and "block shards" in out
+    ref = reference_image(cvr, "manix", W, H, (1, 1), iters)
+    assert ref.max() > 0
+    assert_pixels_close(img, ref, iters, f"CLI --devices {devices} vs one context")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["regenerationSK", "streamingSK"])
+def test_cli_tile_shards_equal_tile_loop(cvr, tmp_path, kernel):
+    """--number-of-tiles 4 2 over three contexts: tiles 0, 3, 6 / 1, 4, 7 / 2, 5,
+    each with its sequential-loop seed (regenerationSK +n_paths, streamingSK +1
+    per tile), against the one-context tile loop."""
+    W, H, iters = 256, 128, 3
+    img, out = run_cli(tmp_path, "tiles", "--synthetic", "hetvol", "-r", str(W), str(H), "-i", str(iters),
+                       "--number-of-tiles", "4", "2", "-k", kernel, "--devices", "0,0,0")
+    assert "tile k -> context k mod N" in out
+    ref = reference_image(cvr, "hetvol", W, H, (4, 2), iters, kernel)
+    assert_pixels_close(img, ref, iters, f"CLI tiles x3 {kernel} vs tile loop")
+
+
+@pytest.mark.gpu
+def test_cli_ragged_tiles_leave_remainder_black(cvr, tmp_path):
+    """Q1 on the multi-device path: 3 x 2 tiles of a 100 x 70 image render
+    tiles of 33 x 35, pixels x >= 99 are never written (zero), the rest equal
+    the one-context tile loop; a one-tile image whose sides are not multiples
+    of 8 cannot be block-sharded and renders on the first device."""
+    img, _ = run_cli(tmp_path, "ragged", "--synthetic", "bucky", "-r", "100", "70", "-i", "2",
+                     "--number-of-tiles", "3", "2", "--devices", "0,0")
+    ref = reference_image(cvr, "bucky", 100, 70, (3, 2), 2)
+    assert (img[:, 99:] == 0).all()
+    assert_pixels_close(img, ref, 2, "ragged tiles x2")
+    img1, out = run_cli(tmp_path, "one", "--synthetic", "bucky", "-r", "100", "70", "-i", "2", "--devices", "0,0")
+    assert "rendering on device 0" in out
+    assert_pixels_close(img1, reference_image(cvr, "bucky", 100, 70, (1, 1), 2), 2, "fallback single device")
+
+
+def test_cli_rejects_bad_devices(tmp_path):
+    """Host-only: an empty --devices list is a usage error (exit 2) before any
+    scene or device is touched."""
+    r = subprocess.run([CLI, "--synthetic", "bucky", "--devices", "0", "--interactive", "0", "-o",
+                        str(tmp_path / "x")], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "--devices" in r.stderr

@@ -198,3 +198,25 @@ def test_flush_fallback_copy(cvr):
     finally:
         buf.close()
         c.close()
+
+
+def test_short_host_buffer_rejected(cvr):
+    """ABI 3: cvr_render_frame takes the host buffer's size and rejects one
+    shorter than the tile (CVR_ERR_INVALID) before anything runs: the seed
+    does not advance and the buffer is not written."""
+    scene = cvr.Scene.synthetic("bucky")
+    c, _, _ = _context(cvr, scene, 64, 64, 1)
+    buf = Pinned(64, 64)
+    try:
+        buf.img[:] = -7.0
+        c.set_seed(5)
+        with pytest.raises(cvr.CvrError) as e:
+            c.render_frame(buf.ptr.value, 1, host_floats=64 * 64 * 4 - 1)
+        assert e.value.code == -1 and "floats" in str(e.value)
+        assert c.get_seed() == 5
+        assert (buf.img == -7.0).all()
+        c.render_frame(buf.ptr.value, 1, host_floats=64 * 64 * 4)  # exactly the tile
+        assert c.get_seed() == 5 + 64 * 64
+    finally:
+        buf.close()
+        c.close()

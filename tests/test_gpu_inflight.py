@@ -163,6 +163,7 @@ def test_morton_sorted_track_order_vs_oracle(cvr, oracle_mod, name):
     imgs = []
     for morton in (0, 1):
         c = cvr.Context(0, "streamingSK")
+        c.set_option(cvr.OPT_SCHEDULER, 2)  # the workgroup pool (streamingSK's default is the wave pool)
         c.set_option(cvr.OPT_MORTON, morton)
         c.set_medium(scene.medium)
         iv, r2v = _setup(cvr, c)

@@ -186,12 +186,14 @@ def test_scheduler_knobs_do_not_change_results(cvr, scenes):
     # (chunk, event/refill threshold, grid, scheduler, pool): the single
     # persistent kernel and the wavefront scheduler with pools from 256 slots
     # (hundreds of events/track iterations) up must all give the same result.
-    # sched 0 = persistent kernel (with work orders/queues), 1 = wavefront pair
+    # sched 0 = persistent kernel (with work orders/queues), 1 = wavefront pair, 3 = wave pool, 4 = per item
     for chunk, thresh, grid, sched, pool, order, queues in [
             (128, 56, 0, 0, 1 << 21, 1, 8), (128, 16, 0, 0, 1 << 21, 0, 1), (64, 1, 0, 0, 1 << 21, 1, 3),
             (256, 64, 0, 0, 1 << 21, 1, 1), (32, 8, 7, 0, 1 << 21, 1, 8), (100, 30, 3, 0, 1 << 21, 0, 1),
             (128, 16, 0, 1, 1 << 21, 1, 8), (64, 1, 0, 1, 256, 1, 8), (256, 64, 0, 1, 4096, 1, 8),
-            (32, 8, 7, 1, 1000, 1, 8)]:
+            (32, 8, 7, 1, 1000, 1, 8),
+            # round 5: sched 3 = the wave pool (every id's default), 4 = one path per work-item
+            (128, 56, 0, 3, 1 << 21, 1, 8), (64, 56, 0, 3, 1 << 21, 0, 1), (256, 56, 0, 4, 1 << 21, 1, 8)]:
         ctx, _, _ = make_ctx(cvr, scene, W, H, "regenerationSK")
         ctx.set_option(cvr.OPT_CHUNK, chunk)
         ctx.set_option(cvr.OPT_EVENT_THRESHOLD, thresh)

@@ -46,15 +46,17 @@ for step in "$@"; do
     pmc_d) run pmc_d 120 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_IFETCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_LDS_BANK_CONFLICT --kernel-trace -d "$OUT/pmc_d" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     pmc_e) run pmc_e 90 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES --kernel-trace -d "$OUT/pmc_e" -o run --output-format csv -- python3 "$ROOT/tools/tune.py" --rounds 2 --variants "regenerationSK:" ;;
     # per-scene profiles: prof:SCENE, pmcf:SCENE (FETCH_SIZE), pmcw:SCENE (WRITE_SIZE)
-    prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline ;;
-    pmcf:*) sc=${step#pmcf:}; mkdir -p "$OUT/pmcf_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcf_$sc/libcvr.sha256"; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
-    pmcw:*) sc=${step#pmcw:}; mkdir -p "$OUT/pmcw_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcw_$sc/libcvr.sha256"; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline --no-shard-emulation ;;
+    pmcf:*) sc=${step#pmcf:}; mkdir -p "$OUT/pmcf_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcf_$sc/libcvr.sha256"; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
+    pmcw:*) sc=${step#pmcw:}; mkdir -p "$OUT/pmcw_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcw_$sc/libcvr.sha256"; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
     # VALU issue (tools/valu.py): pmcv:SCENE
     pmcv:*) sc=${step#pmcv:}; mkdir -p "$OUT/pmcv_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcv_$sc/libcvr.sha256"; run pmcv_$sc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
+    # one kernel id's C2 bench line: benchk:KERNEL
+    benchk:*) k=${step#benchk:}; run benchk_$k 400 python3 bench.py --kernel $k --steps 10 --warmup 2 --no-cpu-baseline --no-shard-emulation ;;
     # the driver's default bench line
     benchdef) run benchdef 600 python3 bench.py ;;
     # arbitrary counters on a scene's bench run: pmcx:SCENE:CTR1,CTR2,...
-    pmcx:*) IFS=: read -r _ sc ctrs <<< "$step"; d=pmcx_${sc}_${ctrs//,/_}; mkdir -p "$OUT/$d"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/$d/libcvr.sha256"; run $d 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$OUT/$d" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmcx:*) IFS=: read -r _ sc ctrs <<< "$step"; d=pmcx_${sc}_${ctrs//,/_}; mkdir -p "$OUT/$d"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/$d/libcvr.sha256"; run $d 300 rocprofv3 --pmc ${ctrs//,/ } --kernel-trace -d "$OUT/$d" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
     # A/B of experiment builds: ab:SCENE:ROUNDS:variant1,variant2,...
     ab:*) IFS=: read -r _ sc rounds vs <<< "$step"; run ab_$sc 400 bash tools/ab.sh $sc $rounds ${vs//,/ } ;;
     *) echo "unknown step $step" ;;
