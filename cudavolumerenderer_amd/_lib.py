@@ -30,7 +30,7 @@ OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1,
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
 OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT, OPT_FRAME_FLUSH = 18, 19, 20, 22, 23, 24
-OPT_UNIFORM_ALBEDO = 25
+OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR = 25, 26
 
 
 class CvrError(RuntimeError):
@@ -146,6 +146,9 @@ def load() -> C.CDLL:
         "cvr_device_info": (I32, [P, C.POINTER(I32), C.POINTER(I32)]),
         "cvr_render_image": (I32, [P, C.POINTER(RenderDesc), P, FP, C.POINTER(Stats)]),
         "cvr_render_tiles": (I32, [P, C.POINTER(RenderDesc), U32, U32, P, FP, C.POINTER(Stats)]),
+        "cvr_render_share_to_host": (I32, [P, C.POINTER(RenderDesc), U32, U32, P, C.c_size_t, C.POINTER(Stats)]),
+        "cvr_host_alloc": (I32, [C.c_size_t, C.POINTER(C.c_void_p)]),
+        "cvr_host_free": (I32, [P]),
         "cvr_default_camera": (I32, [U32, U32, FP, FP]),
         "cvr_tiling": (I32, [U32, U32, U32, U32, C.POINTER(U32)]),
         "cvr_tile_origin": (I32, [U32, U32, C.POINTER(U32), C.POINTER(U32)]),
@@ -538,6 +541,21 @@ class Context:
         self._c(load().cvr_frame_flush_info(self._h, C.byref(b), C.byref(f)))
         return b.value, f.value
 
+    def render_share_to_host(self, host_ptr: int, host_floats: int, width, height, n_tiles=(1, 1), iterations=20,
+                             first_tile: int = 0, tile_stride: int = 1):
+        """One device's share of a multi-device render (cvr_render_share_to_host):
+        tiles first_tile, first_tile + tile_stride, ... (more than one tile), else
+        this context's block shard, stored normalised into the full pinned host
+        image at host_ptr (width*height*4 floats, e.g. a PinnedImage)."""
+        d = RenderDesc()
+        d.resolution[:] = (width, height)
+        d.n_tiles[:] = n_tiles
+        d.iterations = iterations
+        st = Stats()
+        self._c(load().cvr_render_share_to_host(self._h, C.byref(d), first_tile, tile_stride, C.c_void_p(host_ptr),
+                                                host_floats, C.byref(st)))
+        return st
+
     def render_tiles(self, width, height, n_tiles=(1, 1), iterations=20, first_tile: int = 0,
                      tile_stride: int = 1, device_image: Optional[int] = None, host: bool = True):
         """Tiles first_tile, first_tile + tile_stride, ... of render_image's
@@ -569,3 +587,21 @@ class Context:
 
     def __exit__(self, *a):
         self.close()
+
+
+class PinnedImage:
+    """A width x height float4 image in pinned, device-mapped host memory
+    (cvr_host_alloc), viewed as a numpy array; every device can store into it."""
+
+    def __init__(self, width: int, height: int):
+        self.ptr = C.c_void_p()
+        rc = load().cvr_host_alloc(width * height * 16, C.byref(self.ptr))
+        if rc != 0:
+            raise CvrError(rc, load().cvr_last_error(None).decode())
+        self.floats = width * height * 4
+        self.array = np.ctypeslib.as_array(C.cast(self.ptr, C.POINTER(C.c_float)), shape=(height, width, 4))
+
+    def close(self):
+        if self.ptr:
+            load().cvr_host_free(self.ptr)
+            self.ptr = C.c_void_p()

@@ -141,6 +141,7 @@ struct cvr_ctx {
   // 0 = the default, 5 (dense and sparse, split slots)
   int wpool_waves = 0;
   int morton = 0;  // CVR_OPT_MORTON
+  int wave_pair = 0;  // CVR_OPT_WAVE_PAIR
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
@@ -1206,6 +1207,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       // takes effect at the next cvr_set_medium
       c->use_cells = v != 0;
       return CVR_OK;
+    case CVR_OPT_WAVE_PAIR:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "wave pair must be 0 or 1");
+      c->wave_pair = (int)v;
+      return CVR_OK;
     case CVR_OPT_UNIFORM_ALBEDO:
       // takes effect at the next cvr_set_medium
       c->uniform_albedo = v != 0;
@@ -1387,7 +1392,7 @@ int cvr_launch_render(cvr_ctx* c) {
                        4 * cvr::kFrameFlushers);
       L.frame_done = c->frame_done_active;
     }
-    HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream));
+    HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream, c->wave_pair != 0));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }
@@ -1763,6 +1768,7 @@ static void copy_settings(cvr_ctx* d, const cvr_ctx* s) {
   d->pool_tail = s->pool_tail;
   d->wpool_waves = s->wpool_waves;
   d->morton = s->morton;
+  d->wave_pair = s->wave_pair;
   d->swap_batch = s->swap_batch;
   d->scheduler = s->scheduler;
   d->waves = s->waves;

@@ -127,8 +127,8 @@ __device__ __forceinline__ V3 normal_of(uint32_t c) {
   return c == 0u ? mk3(0, 0, 0) : c <= 2u ? mk3(s, 0, 0) : c <= 4u ? mk3(0, s, 0) : mk3(0, 0, s);
 }
 
-template <int kSlots>
-__device__ __forceinline__ void store_full(WavePool<kSlots>& S, float4* __restrict__ gT, uint32_t s,
+template <class Pool>
+__device__ __forceinline__ void store_full(Pool& S, float4* __restrict__ gT, uint32_t s,
                                            const PathState& ps, const Isect& is, uint32_t nseg) {
   S.a[s] = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
   S.b[s] = make_float4(ps.d.x, ps.d.y, ps.d.z, is.dist);
@@ -137,8 +137,8 @@ __device__ __forceinline__ void store_full(WavePool<kSlots>& S, float4* __restri
   S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
   gstore4(gT + s, make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id)));
 }
-template <int kSlots>
-__device__ __forceinline__ void load_full(const WavePool<kSlots>& S, const float4* __restrict__ gT, uint32_t s,
+template <class Pool>
+__device__ __forceinline__ void load_full(const Pool& S, const float4* __restrict__ gT, uint32_t s,
                                           PathState& ps, Isect& is, uint32_t& nseg, float& t) {
   const float4 f = gload4(gT + s);
   const float4 a = S.a[s], b = S.b[s];
@@ -156,15 +156,15 @@ __device__ __forceinline__ void load_full(const WavePool<kSlots>& S, const float
   is.inside = (meta & 8u) != 0u;
   nseg = meta >> 4;
 }
-template <int kSlots>
-__device__ __forceinline__ void store_track(WavePool<kSlots>& S, uint32_t s, float t, const Rng& rng) {
+template <class Pool>
+__device__ __forceinline__ void store_track(Pool& S, uint32_t s, float t, const Rng& rng) {
   S.a[s].w = t;
   S.c[s] = make_uint4(rng.v0, rng.v1, rng.v2, rng.v3);
   S.e[s] = make_uint2(rng.v4, rng.d);
 }
 // Track state of a ready path: o, t, d, max_t, rng.
-template <int kSlots>
-__device__ __forceinline__ void load_track(const WavePool<kSlots>& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
+template <class Pool>
+__device__ __forceinline__ void load_track(const Pool& S, uint32_t s, V3& o, V3& d, Rng& rng, float& t,
                                            float& max_t) {
   const float4 a = S.a[s], b = S.b[s];
   const uint4 c = S.c[s];
@@ -194,8 +194,8 @@ enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
 #ifndef CVR_WPOOL_SPLAT_COMBINE
 #define CVR_WPOOL_SPLAT_COMBINE 1
 #endif
-template <int kSlots>
-__device__ __forceinline__ void splat_wave(WavePool<kSlots>& S, const LaunchParams& L, const PathState& ps, bool esc,
+template <class Pool>
+__device__ __forceinline__ void splat_wave(Pool& S, const LaunchParams& L, const PathState& ps, bool esc,
                                            uint32_t s, uint32_t lane) {
 #if defined(CVR_DIAG_NO_SPLAT)  // diagnostic timing builds only (wrong images): no framebuffer writes
   (void)S; (void)L; (void)ps; (void)esc; (void)s; (void)lane;
@@ -977,6 +977,460 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   }
 }
 
+// ---- workgroup-shared event lists (CVR_OPT_WAVE_PAIR 1, round 5) ------------
+// The round-3/4 verdicts' "event list shared by the waves of a workgroup": two
+// waves per workgroup, one unified slot array (2 x kPairSlots paths), each wave
+// with its own track-ready ring, new-path stack and queue cursor (wave-uniform
+// scalars, as k_wpool), but ONE boundary list and ONE collision list for both:
+// 256-entry LDS rings that either wave files into (ds_add_rtn on the list's
+// tail reserves the entries) and either wave takes a batch from (a CAS on the
+// packed heads claims them; entries are 0xFF until written, so a taker that
+// meets a reserved but unwritten entry waits for it).  A batch thus sees both
+// waves' events, so kind-major batches (48 boundary / 24 collision events of
+// one kind) fill twice as fast.  A path that a wave takes from the shared lists
+// becomes that wave's: it goes to its ready ring, to the shared boundary list or
+// to its new-path stack.  Dense media with cells and brick bounds only (C2 /
+// C3), no in-launch output, no records.  The same walk, the same per-path
+// results: only which wave runs which event changes.
+template <int kWaves>
+struct PairSize {
+  // LDS bytes per two-wave workgroup: twice a one-wave workgroup's budget
+  static constexpr int kBudget = 2 * (163840 / (4 * kWaves) / kLdsGranule * kLdsGranule);
+  static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
+  static constexpr int kHeader = 2 * (4 * STAT_COUNT + 8 + 12 + 4) + 16;
+  // unified slots of the pair: 60 bytes of path state each + a ready-ring and a
+  // new-path-stack entry per wave (a wave may come to own every slot)
+  static constexpr int value = (kBudget - kParams - kHeader - 512) / 64;
+  static_assert(value <= 254, "slot ids are u8 with 0xFF as the empty ring entry");
+};
+template <int kN>
+struct PairPool {
+  float4 a[kN], b[kN];
+  uint4 c[kN];
+  uint2 e[kN];
+  uint32_t meta[kN];
+  uint8_t ready[2][kN];  // each wave's ring of track-ready slots
+  uint8_t ln[2][kN];     // each wave's stack of slots waiting for a new path
+  uint8_t lb[256];       // shared ring of boundary events (0xFF: not written yet / taken)
+  uint8_t lc[256];       // shared ring of real collisions
+  uint32_t tail[2];      // lb, lc tails (entries reserved so far)
+  uint32_t heads;        // lb head | lc head << 16 (mod 2^16; claimed by CAS)
+  uint32_t cnt[2][STAT_COUNT];
+  unsigned long long dead[2];
+  uint32_t cur[2][3];
+  uint32_t pad[2];
+};
+// events of list k (0 boundary, 1 collision) reserved and not yet claimed
+__device__ __forceinline__ uint32_t pair_avail(uint32_t heads, uint32_t tail, uint32_t k) {
+  return (tail - (heads >> (16 * k))) & 0xFFFFu;
+}
+
+template <bool kScatterEps, int kWaves, int kMed>
+__global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchParams Lk) {
+  static_assert(kMed == kMedDenseFull || kMed == kMedDenseFullUniform, "paired waves: dense media with cells and bounds");
+  constexpr int kN = PairSize<kWaves>::value;  // unified slots of the pair
+  MediumParams m = mk;
+  m.leaves = nullptr;
+  m.leaf_density = nullptr;
+  m.leaf_albedo = nullptr;
+  m.sbounds = nullptr;
+  __builtin_assume(m.cells != nullptr);
+  __builtin_assume(m.bounds != nullptr);
+  m.albedo_uniform = kMed == kMedDenseFullUniform ? 1u : 0u;
+  static_assert(sizeof(PairPool<kN>) + sizeof(LaunchParams) <= (size_t)PairSize<kWaves>::kBudget,
+                "paired pool exceeds the LDS budget of kWaves waves per SIMD");
+  __shared__ PairPool<kN> S;
+  __shared__ LaunchParams L;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x == 0) {
+    L = Lk;
+    S.tail[0] = S.tail[1] = 0u;
+    S.heads = 0u;
+  }
+  for (uint32_t i = threadIdx.x; i < 256u; i += 128u) {
+    S.lb[i] = 0xFFu;
+    S.lc[i] = 0xFFu;
+  }
+  uint32_t c_steps = 0, c_fetch = 0;
+  if (lane < (uint32_t)STAT_COUNT) S.cnt[wv][lane] = 0u;
+  if (lane == 0) {
+    S.dead[wv] = 0ull;
+    S.cur[wv][0] = S.cur[wv][1] = 0u;
+  }
+  __syncthreads();
+  uint32_t n_over = 0;
+  if (lane == 0) {
+    const uint32_t vw = 2u * blockIdx.x + wv;  // the wave's index as a one-wave launch would number it
+    S.cur[wv][2] = (((__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % (L.n_queues / L.sub)) * L.sub +
+                    (vw >> 4) % L.sub)
+                   << 8;
+  }
+  const uint32_t batch = L.batch;
+  uint32_t ready_head = 0, n_ready = 0;
+  // this wave's half of the slots starts free
+  uint32_t n_ln = kN / 2;
+  for (uint32_t i = lane; i < (uint32_t)kN / 2; i += 64u) S.ln[wv][i] = (uint8_t)(wv * (kN / 2) + i);
+  float4* __restrict__ gT = L.pool_T + (size_t)blockIdx.x * kN;  // the pair's event-only slot part
+
+  // File lanes' slots into the shared lists: mb boundary, mc collision lanes.
+  // The slot's LDS state is written before: the release fence orders it (and
+  // the wave's pool_T stores) before the list entries the other wave may read.
+  auto file_shared = [&](bool is_b, bool is_c, uint32_t s) {
+    const unsigned long long mb = __ballot(is_b), mc = __ballot(is_c);
+    const uint32_t kb = (uint32_t)__popcll(mb), kc = (uint32_t)__popcll(mc);
+    if ((kb | kc) == 0u) return;
+    uint32_t tb0 = 0, tc0 = 0;
+    if (lane == 0) {
+      if (kb) tb0 = __hip_atomic_fetch_add(&S.tail[0], kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (kc) tc0 = __hip_atomic_fetch_add(&S.tail[1], kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    tb0 = __builtin_amdgcn_readfirstlane(tb0);
+    tc0 = __builtin_amdgcn_readfirstlane(tc0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (is_b) S.lb[(tb0 + lane_rank(mb)) & 255u] = (uint8_t)s;
+    if (is_c) S.lc[(tc0 + lane_rank(mc)) & 255u] = (uint8_t)s;
+  };
+
+  for (;;) {
+    __builtin_amdgcn_s_setprio(kPrioTrack);
+    int slot = -1;
+    int fst = 0;
+    V3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
+    Rng rng{0, 0, 0, 0, 0, 0};
+    float t = 0.0f, max_t = 0.0f;
+    for (;;) {
+      const unsigned long long trk = (__ballot(slot >= 0) & __ballot(fst == 0));
+      const uint32_t n_trk = (uint32_t)__popcll(trk);
+      if (64u - n_trk >= batch || n_trk == 0u) {
+        if (fst == 2 && !(t < max_t)) fst = 3;
+        if (fst != 0) store_track(S, (uint32_t)slot, t, rng);
+        n_over += (uint32_t)__popcll(__ballot(fst == 1));
+        file_shared((fst & 1) != 0, fst == 2, (uint32_t)slot);
+        if (fst != 0) {
+          slot = -1;
+          fst = 0;
+        }
+        const unsigned long long idle = __ballot(slot < 0);
+        const uint32_t k = min((uint32_t)__popcll(idle), n_ready), rank = lane_rank(idle);
+        if (slot < 0 && rank < k) {
+          const uint32_t r = ready_head + rank;
+          const uint32_t s = S.ready[wv][r >= (uint32_t)kN ? r - kN : r];
+          slot = (int)s;
+          load_track(S, s, o, d, rng, t, max_t);
+        }
+        ready_head += k;
+        if (ready_head >= (uint32_t)kN) ready_head -= kN;
+        n_ready -= k;
+      }
+      const uint32_t n_act = (uint32_t)__popcll((__ballot(slot >= 0) & __ballot(fst == 0)));
+      const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0));
+      const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);
+      const uint32_t n_shared = pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
+                                pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1);
+      if (n_shared + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
+        if (fst == 2 && !(t < max_t)) fst = 3;
+        if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
+        const unsigned long long mr = (__ballot(slot >= 0) & __ballot(fst == 0));
+        if (slot >= 0 && fst == 0) S.ready[wv][(ready_head + n_ready + lane_rank(mr)) % kN] = (uint8_t)slot;
+        n_over += (uint32_t)__popcll(__ballot(fst == 1));
+        n_ready += (uint32_t)__popcll(mr);
+        file_shared((fst & 1) != 0, fst == 2, (uint32_t)slot);
+        break;
+      }
+#pragma unroll
+      for (int u = 0; u < CVR_WPOOL_UNROLL / kLook; ++u) {
+        if (slot >= 0 && fst == 0) {
+          float tk[kLook], xtk[kLook];
+          uint32_t sva[kLook], svb[kLook];
+          WoodcockPoint Pk[kLook];
+          float tt = t;
+#pragma unroll
+          for (int k = 0; k < kLook; ++k) {
+            const float xi = rng_float(rng);
+            xtk[k] = rng_float(rng);
+            sva[k] = rng.v0;
+            svb[k] = rng.v1;
+            tt = woodcock_advance(m, xi, tt);
+            tk[k] = tt;
+          }
+#pragma unroll
+          for (int k = 0; k < kLook; ++k) Pk[k] = woodcock_point(m, o, d, tk[k]);
+          int end = kLook;
+#pragma unroll
+          for (int k = 0; k < kLook; ++k) {
+            if (end == kLook) {
+              if (!(tk[k] <= max_t)) {
+                fst = 1;
+                end = k;
+              } else if (!(Pk[k].qb < xtk[k])) {
+                ++c_fetch;
+                const float rho = m.scale * woodcock_density(m, Pk[k]);
+                if (!(rho * m.inv_sigma < xtk[k])) {
+                  fst = 2;
+                  end = k;
+                }
+              }
+            }
+          }
+          c_steps += end == kLook ? kLook : end + 1;
+          t = tk[kLook - 1];
+#pragma unroll
+          for (int k = 0; k < kLook - 1; ++k)
+            if (end == k) t = tk[k];
+          if (end < kLook - 1) {
+            uint32_t w[2 * kLook + 5];
+#pragma unroll
+            for (int k = 0; k < kLook - 1; ++k) {
+              w[2 * k + 2] = sva[k];
+              w[2 * k + 3] = svb[k];
+            }
+            w[2 * kLook] = rng.v0;
+            w[2 * kLook + 1] = rng.v1;
+            w[2 * kLook + 2] = rng.v2;
+            w[2 * kLook + 3] = rng.v3;
+            w[2 * kLook + 4] = rng.v4;
+#pragma unroll
+            for (int j = 1; j < kLook; ++j) {
+              if (end + 1 == j) {
+                rng.v0 = w[2 * j];
+                rng.v1 = w[2 * j + 1];
+                rng.v2 = w[2 * j + 2];
+                rng.v3 = w[2 * j + 3];
+                rng.v4 = w[2 * j + 4];
+              }
+            }
+            rng.d -= (uint32_t)(2 * (kLook - 1 - end)) * 362437u;
+          }
+        }
+      }
+    }
+    // claim the batch's events from the shared lists (kind-major thresholds as k_wpool)
+    __builtin_amdgcn_s_setprio(kPrioEvent);
+    uint32_t tb = 0, tc = 0, hb = 0, hc = 0;
+    {
+      uint32_t h = __builtin_amdgcn_readfirstlane(S.heads);
+      for (;;) {
+        const uint32_t ab = pair_avail(h, __builtin_amdgcn_readfirstlane(S.tail[0]), 0);
+        const uint32_t ac = pair_avail(h, __builtin_amdgcn_readfirstlane(S.tail[1]), 1);
+        if (ab >= (uint32_t)CVR_WPOOL_KIND_MIN) {
+          tb = min(ab, 64u);
+          tc = 0;
+        } else if (ac >= (uint32_t)CVR_WPOOL_KIND_MIN_C) {
+          tb = 0;
+          tc = min(ac, 64u);
+        } else {
+          tb = min(ab, 64u);
+          tc = min(ac, 64u - tb);
+        }
+        if ((tb | tc) == 0u) break;
+        const uint32_t want = ((h + tb) & 0xFFFFu) | (((h >> 16) + tc) << 16);
+        uint32_t got = 0;
+        if (lane == 0) {
+          got = h;
+          __hip_atomic_compare_exchange_strong(&S.heads, &got, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        got = __builtin_amdgcn_readfirstlane(got);
+        if (got == h) break;
+        h = got;  // the other wave claimed first: retry with its heads
+      }
+      hb = h & 0xFFFFu;
+      hc = h >> 16;
+    }
+    const bool any_event = (tb | tc) != 0u;
+    // no path left: nothing to track, nothing shared, no new path to start
+    if (!any_event && n_ready == 0u && (n_ln == 0u || (S.cur[wv][2] & kCurExhausted))) {
+      const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);
+      if (pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
+              pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1) ==
+          0u)
+        break;
+    }
+    MediumParams me = m;
+    me.g = opaque_s(m.g);
+    me.ax = opaque_s(m.ax);
+    me.ay = opaque_s(m.ay);
+    me.eta = opaque_s(m.eta);
+    me.inv_eta = opaque_s(m.inv_eta);
+    me.bmin = mk3(opaque_s(m.bmin.x), opaque_s(m.bmin.y), opaque_s(m.bmin.z));
+    me.bmax = mk3(opaque_s(m.bmax.x), opaque_s(m.bmax.y), opaque_s(m.bmax.z));
+    me.albedo_bg = mk3(opaque_s(m.albedo_bg.x), opaque_s(m.albedo_bg.y), opaque_s(m.albedo_bg.z));
+    {
+      uint32_t tn;
+      if (tb >= (uint32_t)CVR_WPOOL_KIND_MIN) tn = min(n_ln, 64u - tb);
+      else if (tc >= (uint32_t)CVR_WPOOL_KIND_MIN_C) tn = n_ln < 64u ? 0u : min(n_ln, 64u - tc);
+      else tn = min(n_ln, 64u - tb - tc);
+      uint32_t kind = K_NONE, s = 0;
+      if (lane < tb + tc) {
+        // a claimed entry may be reserved but not yet written by the other wave: wait for it
+        uint8_t* q = lane < tb ? &S.lb[(hb + lane) & 255u] : &S.lc[(hc + lane - tb) & 255u];
+        uint32_t v, spins = 0;
+        do {
+          v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } while (v == 0xFFu && ++spins < (1u << 24));
+        // (a bounded wait: an entry that never appears would be a bug; the item is then
+        // dropped and counted as truncated, so the launch ends and the counters differ)
+        __hip_atomic_store(q, (uint8_t)0xFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        s = v;
+        kind = v == 0xFFu ? K_NONE : lane < tb ? K_BOUNDARY : K_COLLIDE;
+        if (v == 0xFFu) atomicAdd(&S.cnt[wv][STAT_TRUNCATED], 1u);
+      } else if (lane < tb + tc + tn) {
+        kind = K_NEW;
+        s = S.ln[wv][n_ln - 1u - (lane - tb - tc)];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the filer's slot state and pool_T stores
+      n_ln -= tn;
+      PathState ps{};
+      Isect is{};
+      uint32_t nseg = 0;
+      float t_hit = 0.0f;
+      bool to_ready = false, to_lb = false, to_ln = false;
+      bool truncated = false, escaped = false, seg_first = false, seg_next = false;
+      const unsigned long long want = __ballot(kind == K_NEW);
+      if (want != 0ull) {
+        const uint32_t rank = lane_rank(want);
+        bool got = false;
+        uint32_t given = 0;
+        uint32_t cnext = __builtin_amdgcn_readfirstlane(S.cur[wv][0]), cend = __builtin_amdgcn_readfirstlane(S.cur[wv][1]);
+        uint32_t cqh = __builtin_amdgcn_readfirstlane(S.cur[wv][2]);
+        while (given < (uint32_t)__popcll(want) && !(cqh & kCurExhausted)) {
+          if (cnext == cend) {
+            uint32_t b = 0xFFFFFFFFu, qsel = 0;
+            if (lane == 0) {
+              unsigned long long dead = S.dead[wv];
+              for (uint32_t k = 0; k < L.n_queues; ++k) {
+                const uint32_t q = ((cqh >> 8) + k) % L.n_queues;
+                if ((dead >> q) & 1ull) continue;
+                const uint32_t g = atomicAdd(L.queue + 16 * q, L.chunk);
+                if (g < queue_units(L, q)) {
+                  b = g;
+                  qsel = q;
+                  break;
+                }
+                dead |= 1ull << q;
+              }
+              S.dead[wv] = dead;
+            }
+            b = __shfl(b, 0);
+            qsel = __shfl(qsel, 0);
+            if (b == 0xFFFFFFFFu) {
+              cqh |= kCurExhausted;
+              break;
+            }
+            cqh = qsel | qsel << 8;
+            cnext = b;
+            cend = min(b + L.chunk, queue_units(L, qsel));
+          }
+          const uint32_t take = min((uint32_t)__popcll(want) - given, cend - cnext);
+          if (kind == K_NEW && rank >= given && rank < given + take) {
+            const uint32_t pid = unit_to_path(L, cqh & 0xFFu, cnext + (rank - given));
+            path_begin(L, pid, ps);
+            is.normal = mk3(0, 0, 0);
+            nseg = 0;
+            got = true;
+          }
+          cnext += take;
+          given += take;
+        }
+        if (lane == 0) {
+          S.cur[wv][0] = cnext;
+          S.cur[wv][1] = cend;
+          S.cur[wv][2] = cqh;
+        }
+        const uint32_t n_got = (uint32_t)__popcll(__ballot(got));
+        if (lane == 0) S.cnt[wv][STAT_PATHS] += n_got;
+        if (got) {
+          if (L.max_segments && nseg >= L.max_segments) {
+            truncated = true;
+            to_ln = true;
+          } else {
+            ++nseg;
+            seg_first = true;
+            if (!aabb_intersect(me, ps.o, ps.d, is)) {
+              escaped = true;
+              to_ln = true;
+            } else if (is.inside) {
+              store_full(S, gT, s, ps, is, nseg);
+              to_ready = true;
+            } else {
+              kind = K_BOUNDARY;
+            }
+          }
+        }
+      }
+      const bool filed = lane < tb + tc && kind != K_NONE;  // (K_NONE: a dropped entry, see above)
+      if (filed) load_full(S, gT, s, ps, is, nseg, t_hit);
+      if (filed && lane < tb && !(t_hit <= is.dist)) rng_undo(ps.rng);
+      bool alive = false;
+      if (kind == K_BOUNDARY) {
+        boundary_event(me, ps, is);
+        alive = roulette(ps);
+      }
+      if (kind == K_COLLIDE) {
+        scatter_event<kScatterEps>(me, ps, t_hit);
+        alive = roulette(ps);
+      }
+      const uint32_t n_alb = (uint32_t)__popcll(__ballot(kind == K_COLLIDE));
+      if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) to_ln = true;
+      if (alive) {
+        if (L.max_segments && nseg >= L.max_segments) {
+          truncated = true;
+          to_ln = true;
+        } else {
+          ++nseg;
+          seg_next = true;
+          if (!aabb_intersect(me, ps.o, ps.d, is)) {
+            escaped = true;
+            to_ln = true;
+          } else {
+            store_full(S, gT, s, ps, is, nseg);
+            to_ready = is.inside;
+            to_lb = !is.inside;
+          }
+        }
+      }
+      splat_wave(S, L, ps, escaped, s, lane);
+      {
+        const uint32_t n_seg = (uint32_t)(__popcll(__ballot(seg_first)) + __popcll(__ballot(seg_next)));
+        const uint32_t n_esc = (uint32_t)__popcll(__ballot(escaped)), n_tr = (uint32_t)__popcll(__ballot(truncated));
+        if (lane == 0) {
+          S.cnt[wv][STAT_SEGMENTS] += n_seg;
+          S.cnt[wv][STAT_ALBEDO] += n_alb;
+          S.cnt[wv][STAT_ESCAPED] += n_esc;
+          S.cnt[wv][STAT_TRUNCATED] += n_tr;
+        }
+      }
+      const unsigned long long mr = __ballot(to_ready), mn = __ballot(to_ln);
+      if (to_ready) S.ready[wv][(ready_head + n_ready + lane_rank(mr)) % kN] = (uint8_t)s;
+      if (to_ln) S.ln[wv][n_ln + lane_rank(mn)] = (uint8_t)s;
+      n_ready += (uint32_t)__popcll(mr);
+      n_ln += (uint32_t)__popcll(mn);
+      file_shared(to_lb, false, s);
+    }
+    if (S.cur[wv][2] & kCurExhausted) {
+      const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);
+      const uint32_t n_live = n_ready + pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
+                              pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1);
+      const uint32_t dr = fresh(L).drain;
+      n_ln = dr ? 64u - min(64u, (n_live * dr + dr) / (dr + 1u)) : 0u;
+    }
+  }
+  {
+    unsigned long long steps = c_steps, fetch = c_fetch;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      steps += __shfl_xor(steps, off);
+      fetch += __shfl_xor(fetch, off);
+    }
+    const unsigned long long w[STAT_COUNT] = {S.cnt[wv][STAT_PATHS], S.cnt[wv][STAT_SEGMENTS], steps, steps - n_over,
+                                              S.cnt[wv][STAT_ALBEDO], S.cnt[wv][STAT_ESCAPED], S.cnt[wv][STAT_TRUNCATED],
+                                              fetch};
+    if (lane < (uint32_t)STAT_COUNT && w[lane])
+      __hip_atomic_fetch_add(gmem(L.stats + lane), w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // Instances: 5 waves per SIMD (the default budget) for every medium layout, with and
 // without the in-launch output; the other budgets for the generic layouts.
 template <bool E>
@@ -1006,13 +1460,24 @@ static const void* wpool_record_fn(int waves, bool sparse) {
 }
 
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
-                        hipStream_t s) {
+                        hipStream_t s, bool pair) {
   if (L.path_count == 0) return hipSuccess;
   const bool sparse = m.leaves != nullptr;
   const bool flush = L.frame_done != nullptr;
   const bool full = !sparse && m.cells != nullptr && m.bounds != nullptr;
   const bool uniform = m.albedo_uniform != 0u;
   if (L.rec && flush) return hipErrorInvalidValue;
+  if (pair && waves == 5 && full && !flush && !L.rec && grid >= 2) {
+    // paired waves (workgroup-shared event lists): two waves per workgroup
+#define CVR_WPAIR(E, M) reinterpret_cast<const void*>(&k_wpair<E, 5, M>)
+    const void* fn = scatter_eps ? (uniform ? CVR_WPAIR(true, kMedDenseFullUniform) : CVR_WPAIR(true, kMedDenseFull))
+                                 : (uniform ? CVR_WPAIR(false, kMedDenseFullUniform) : CVR_WPAIR(false, kMedDenseFull));
+#undef CVR_WPAIR
+    MediumParams mm = m;
+    LaunchParams ll = L;
+    void* args[] = {&mm, &ll};
+    return hipLaunchKernel(fn, dim3(grid / 2), dim3(128), args, 0, s);
+  }
   const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
                          : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush, uniform)
                                         : wpool_fn<false>(waves, sparse, full, flush, uniform));

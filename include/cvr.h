@@ -142,6 +142,11 @@ typedef enum {
                                  ended (cvr_frame_flush_info); 0 normalise + copy after the launch.
                                  Same image either way (C2: 5.14 vs 5.29 ms per call).  2 (tests):
                                  the flushers give up at once, so the call takes its fallback copy. */
+  CVR_OPT_WAVE_PAIR = 26,      /* wave-pool scheduler, dense media with cells and bounds: 1 runs two waves
+                                 per workgroup whose boundary and collision event lists are shared
+                                 (k_wpair: either wave files into them and runs a batch from them; round
+                                 5); 0 (default) one wave per workgroup, private lists.
+                                 Scheduling only: results are unchanged. */
   /* 21: unused (a drain-time path migration between waves, measured slower: DESIGN.md §6) */
   CVR_OPT_DRAIN = 22,          /* wave-pool scheduler, once the queues are empty: an event batch runs as
                                  soon as the waiting segments x d >= the tracking ones (d = 0: only when

@@ -100,3 +100,49 @@ def test_cli_rejects_bad_devices(tmp_path):
     r = subprocess.run([CLI, "--synthetic", "bucky", "--devices", "0", "--interactive", "0", "-o",
                         str(tmp_path / "x")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 2 and "--devices" in r.stderr
+
+
+@pytest.mark.gpu
+def test_share_to_host_from_python_threads(cvr):
+    """The same multi-device path through the Python binding: three contexts
+    (sharing one device medium), one Python thread each (ctypes releases the
+    GIL), block shards of one tile into one PinnedImage."""
+    import threading
+    W, H, iters = 128, 128, 3
+    scene = cvr.Scene.synthetic("hetvol")
+    iv, r2v = cvr.default_camera(W, H)
+    ctxs = []
+    for k in range(3):
+        c = cvr.Context(0, "regenerationSK")
+        if k == 0:
+            c.set_medium(scene.medium)
+        else:
+            c.share_medium(ctxs[0])
+        c.set_camera(iv, r2v, (W, H))
+        c.init()
+        c.set_block_shard(k, 3)
+        ctxs.append(c)
+    img = cvr.PinnedImage(W, H)
+    try:
+        img.array[:] = -1.0
+        errs = []
+
+        def work(k):
+            try:
+                ctxs[k].render_share_to_host(img.ptr.value, img.floats, W, H, (1, 1), iters)
+            except Exception as e:  # noqa: BLE001 (reported below)
+                errs.append(e)
+        th = [threading.Thread(target=work, args=(k,)) for k in range(3)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        out = img.array.copy()
+    finally:
+        img.close()
+    assert (out != -1.0).all(), "a pixel no share wrote"
+    for c in reversed(ctxs):
+        c.close()
+    ref = reference_image(cvr, "hetvol", W, H, (1, 1), iters)
+    assert_pixels_close(out[..., :3], ref, iters, "python threads x3 vs one context")

@@ -4,7 +4,7 @@
 set -eu
 cd "$(dirname "$0")/.."
 F=gpurun_out/final
-P=${1:-profiles/round4}
+P=${1:-profiles/round5}
 for sc in manix hetvol cloud; do
   case $sc in manix) key=k_wpool_1024x1024_20it; c=c2;; hetvol) key=hetvol_k_wpool_1024x1024_20it; c=c3;;
                      cloud) key=cloud_k_wpool_4096x4096_20it; c=c5;; esac
@@ -13,8 +13,8 @@ for sc in manix hetvol cloud; do
               cloud) inst="k_wpool<false, 5, 1, false, false>";; esac
   python3 tools/valu.py $F/pmcv_$sc $key "$inst" | cut -c1-140
   cp $F/prof_$sc/run_kernel_stats.csv $P/${c}_kernel_stats.csv
-  if [ $sc = cloud ]; then sw="3 1"; else sw="10 2"; fi
-  python3 tools/kernel_phases.py $F/prof_$sc/run_kernel_trace.csv "$inst" $sw $P/${c}_kernel_phases.json | grep _ms
+  if [ $sc = cloud ]; then sw="3 1"; else sw="20 5"; fi
+  python3 tools/kernel_phases.py $F/prof_$sc/run_kernel_trace.csv "$inst" $sw $P/${c}_kernel_phases.json $F/prof_$sc.log | grep "_ms\|_over_"
 done
 python3 tools/pmc_summary.py $P/pmc_k_wpool.json k_wpool $F/pmc_a $F/pmc_b $F/pmc_c $F/pmc_d
 python3 tools/pmc_summary.py $P/pmc_k_wpool_cloud.json k_wpool $F/pmc5_a $F/pmc5_b $F/pmc5_c

@@ -22,8 +22,10 @@ B="python3 bench.py --no-cpu-baseline"
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 600 python3 -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider
 for sc in manix hetvol cloud; do
-  if [ $sc = cloud ]; then S="--steps 3 --warmup 1"; else S="--steps 10 --warmup 2"; fi
-  # no shard emulation in the traced run: tools/kernel_phases.py reads the bench's own launches
+  # the driver's own bench settings (--steps 20 --warmup 5) for C2/C3, so the traced pipelined
+  # phase is the headline step; no shard emulation in the traced run: tools/kernel_phases.py
+  # reads the bench's own launches and compares their span with the run's ms_per_step
+  if [ $sc = cloud ]; then S="--steps 3 --warmup 1"; else S="--steps 20 --warmup 5"; fi
   step prof_$sc 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- $B --no-shard-emulation --scene $sc $S
   if [ $sc = cloud ]; then S="--steps 2 --warmup 1"; else S="--steps 3 --warmup 1"; fi
   step pmcf_$sc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- $B --scene $sc --serial $S

@@ -53,6 +53,10 @@ for step in "$@"; do
     pmcv:*) sc=${step#pmcv:}; mkdir -p "$OUT/pmcv_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcv_$sc/libcvr.sha256"; run pmcv_$sc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
     # one kernel id's C2 bench line: benchk:KERNEL
     benchk:*) k=${step#benchk:}; run benchk_$k 400 python3 bench.py --kernel $k --steps 10 --warmup 2 --no-cpu-baseline --no-shard-emulation ;;
+    # in-process interleaved variants: tunev:SCENE:ROUNDS:variant;variant (e.g. regenerationSK:pair=1)
+    tunev:*) IFS=: read -r _ sc rounds vs <<< "$step"; run tunev_$sc 400 python3 tools/tune.py --scene $sc --rounds $rounds --variants ${vs//;/ } ;;
+    # selected GPU test files: pytestf:tests/a.py,tests/b.py
+    pytestf:*) fs=${step#pytestf:}; run pytestf 900 python3 -u -m pytest ${fs//,/ } -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
     # the driver's default bench line
     benchdef) run benchdef 600 python3 bench.py ;;
     # arbitrary counters on a scene's bench run: pmcx:SCENE:CTR1,CTR2,...

@@ -7,7 +7,10 @@ timed phases (tools/final_profile.sh):
   serial     warmup + steps launches one at a time: the average dispatch
              duration is the kernel's own time, which bench.py's
              roofline.kernel_ms measures with HIP events.
-  python tools/kernel_phases.py TRACE.csv KERNEL_SUBSTR STEPS WARMUP [OUT.json]"""
+  python tools/kernel_phases.py TRACE.csv KERNEL_SUBSTR STEPS WARMUP [OUT.json [BENCH.log]]
+BENCH.log: the profiled bench run's own output; its JSON line's ms_per_step (the
+pipelined step as that run timed it, profiler included) is reported beside the
+trace's amortized span per launch, which it should match."""
 import csv
 import json
 import sys
@@ -30,6 +33,13 @@ def main():
            "note": "serial = one launch at a time (bench.py roofline.kernel_ms); pipelined dispatches overlap, "
                    "so their per-dispatch durations include their neighbours' time: the amortized time per "
                    "launch is the span of the timed dispatches / steps"}
+    if len(sys.argv) > 6:
+        for line in open(sys.argv[6]):
+            if line.startswith("{"):
+                b = json.loads(line)
+                out["profiled_run_ms_per_step"] = b["ms_per_step"]
+                out["profiled_run_kernel_ms"] = b["roofline"]["kernel_ms"]
+                out["span_per_launch_over_step"] = out["pipelined_span_per_launch_ms"] / b["ms_per_step"]
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 5:
         json.dump(out, open(sys.argv[5], "w"), indent=1)

@@ -98,6 +98,8 @@ def main():
             c.set_option(cvr.OPT_MORTON, d["morton"])
         if "pool" in d:
             c.set_option(cvr.OPT_POOL, d["pool"])
+        if "pair" in d:
+            c.set_option(cvr.OPT_WAVE_PAIR, d["pair"])
         c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
         c.init()
         c.set_resolution(W, H)
