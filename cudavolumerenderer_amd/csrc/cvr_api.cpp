@@ -142,6 +142,7 @@ struct cvr_ctx {
   int wpool_waves = 0;
   int morton = 0;  // CVR_OPT_MORTON
   int wave_pair = 0;  // CVR_OPT_WAVE_PAIR
+  int sample_order = 0;  // CVR_OPT_SAMPLE_ORDER
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
@@ -1207,6 +1208,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       // takes effect at the next cvr_set_medium
       c->use_cells = v != 0;
       return CVR_OK;
+    case CVR_OPT_SAMPLE_ORDER:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "sample order must be 0 or 1");
+      c->sample_order = (int)v;
+      return CVR_OK;
     case CVR_OPT_WAVE_PAIR:
       if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "wave pair must be 0 or 1");
       c->wave_pair = (int)v;
@@ -1317,7 +1322,8 @@ int cvr_launch_render(cvr_ctx* c) {
     L.chunk = per_wave >= 2048 ? 256u : per_wave >= 1024 ? 128u : 64u;
   }
   if (scheduler_for(c) == 3) {
-    L.drain = (uint32_t)(c->drain < 0 ? 1 : c->drain);
+    L.wflags = (uint32_t)(c->drain < 0 ? 1 : c->drain) & cvr::kDrainMask;
+    if (c->sample_order == 1) L.wflags |= cvr::kUnitSampleInner | cvr::kSplatCombine;
   }
   // The persistent schedulers' u32 queue heads run past a queue's end by at
   // most one chunk per wave before every wave sees the queue exhausted
@@ -1755,6 +1761,7 @@ static void copy_settings(cvr_ctx* d, const cvr_ctx* s) {
   d->n_queues = s->n_queues;
   d->subqueues = s->subqueues;
   d->drain = s->drain;
+  d->sample_order = s->sample_order;
   d->order = s->order;
   d->max_segments = s->max_segments;
   d->chunk = s->chunk;

@@ -219,9 +219,10 @@ struct LaunchParams {
   uint32_t batch;         // wave-pool kernel: idle lanes that trigger a swap
   uint32_t naive_mk;      // bit 0: trace kernel runs naiveMK paths (walk_mk) instead of path_begin + loop;
                           // bit 1: pool kernel sorts each track phase's paths by Morton code (streamingSK)
-  // Wave pool, once the queues are empty (the launch's drain): an event batch runs when
-  // waiting x drain >= tracking paths (0: only when no lane tracks or 64 events wait).
-  uint32_t drain;
+  // Wave pool: bits 0-15 the drain rule (once the queues are empty, the launch's drain, an
+  // event batch runs when waiting x drain >= tracking paths; 0: only when no lane tracks or
+  // 64 events wait); kUnitSampleInner, kSplatCombine: see unit_to_path / splat_wave.
+  uint32_t wflags;
   // Work order (scheduling only; results are bound to path ids).  order 0:
   // path ids in sample-major order from one queue.  order 1: 8x8-pixel
   // blocks with all their samples back to back (path_first must be a
@@ -282,17 +283,16 @@ CVR_DEV uint32_t queue_units(const LaunchParams& L, uint32_t q) {
   if (L.order == 0) return q == 0 ? L.path_count : 0u;
   return (queue_blocks_begin(L, q + 1) - queue_blocks_begin(L, q)) * 64u * L.samples;
 }
-// Within a block the units run pixel by pixel with the pixel's samples
-// innermost (round 5, CVR_UNIT_SAMPLE_INNER; before: the 64 pixels of sample
-// 0, then of sample 1, ...), so the paths a wave holds at once belong to a few
-// pixels, and the escapes of one event batch mostly share pixels, whose
-// framebuffer adds the batch then combines (splat_wave).  The pixel of unit
-// rem of a block is rem / samples = (rem << 6) / (64 samples), one fastdiv by
-// the block divisor (exact while 64 * 64 * samples <= 2^32: the host keeps
-// launches with more than 2^20 samples in path-id order).
-#ifndef CVR_UNIT_SAMPLE_INNER
-#define CVR_UNIT_SAMPLE_INNER 1
-#endif
+// Within a block the units run sample by sample, the block's 64 pixels
+// innermost.  With kUnitSampleInner (round 5, CVR_OPT_SAMPLE_ORDER 1) they run
+// pixel by pixel with the pixel's samples innermost instead, so the paths a
+// wave holds at once belong to a few pixels and the escapes of one event batch
+// mostly share pixels, whose framebuffer adds the batch then combines
+// (splat_wave, kSplatCombine).  The pixel of unit rem of a block is then
+// rem / samples = (rem << 6) / (64 samples), one fastdiv by the block divisor
+// (exact while 64 * 64 * samples <= 2^32: the host keeps launches with more
+// than 2^20 samples in path-id order).  Scheduling only: the same path ids.
+constexpr uint32_t kDrainMask = 0xFFFFu, kUnitSampleInner = 1u << 16, kSplatCombine = 1u << 17;
 CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.order == 0) return L.path_first + u;
   const uint32_t per_block = 64u * L.samples;
@@ -301,11 +301,14 @@ CVR_DEV uint32_t unit_to_path(const LaunchParams& L, uint32_t q, uint32_t u) {
   if (L.block_perm) bl = gmem(L.block_perm)[bl];
   const uint32_t b = L.blk_off + __umul24(bl, L.blk_stride);
   const uint32_t rem = u - bq * per_block;
-#if CVR_UNIT_SAMPLE_INNER
-  const uint32_t lane = fastdiv(rem << 6, L.div_block), s = rem - lane * L.samples;
-#else
-  const uint32_t s = rem >> 6, lane = rem & 63u;
-#endif
+  uint32_t s, lane;
+  if (L.wflags & kUnitSampleInner) {
+    lane = fastdiv(rem << 6, L.div_block);
+    s = rem - lane * L.samples;
+  } else {
+    s = rem >> 6;
+    lane = rem & 63u;
+  }
   const uint32_t by = fastdiv(b, L.div_blocks_x);
   const uint32_t px = (b - by * L.blocks_x) * 8u + (lane & 7u), py = by * 8u + (lane >> 3);
   return L.path_first + s * L.tile_px + py * L.tile_w + px;

@@ -176,6 +176,17 @@ __device__ __forceinline__ void load_track(const Pool& S, uint32_t s, V3& o, V3&
   rng = Rng{c.x, c.y, c.z, c.w, e.x, e.y};
 }
 
+// The launch parameters as seen from code that runs rarely (the drain): the
+// LDS address goes through an empty asm each time, so the compiler cannot
+// hoist loads of L's fields out of the main loop and hold them in registers
+// across the track loop (the dense kernel has no VGPR to spare at 5 waves).
+typedef __attribute__((address_space(3))) const LaunchParams LdsParams;
+__device__ __forceinline__ const LaunchParams& fresh(const LaunchParams& L) {
+  LdsParams* p = (LdsParams*)&L;
+  asm volatile("" : "+v"(p));
+  return *(const LaunchParams*)p;
+}
+
 enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
 
 // The batch's escapes, combined per pixel before the framebuffer atomics
@@ -191,19 +202,19 @@ enum : uint32_t { K_BOUNDARY = 0, K_COLLIDE = 1, K_NEW = 2, K_NONE = 3 };
 // additions changes, so the per-pixel bound of DESIGN.md §4 holds: a pixel's
 // n contributions are still summed once each, in some order.  With no pixel
 // escaped to twice the batch splats per lane as before.
-#ifndef CVR_WPOOL_SPLAT_COMBINE
-#define CVR_WPOOL_SPLAT_COMBINE 1
-#endif
-template <class Pool>
+template <bool kCombine, class Pool>
 __device__ __forceinline__ void splat_wave(Pool& S, const LaunchParams& L, const PathState& ps, bool esc,
                                            uint32_t s, uint32_t lane) {
 #if defined(CVR_DIAG_NO_SPLAT)  // diagnostic timing builds only (wrong images): no framebuffer writes
   (void)S; (void)L; (void)ps; (void)esc; (void)s; (void)lane;
   return;
 #endif
-#if CVR_WPOOL_SPLAT_COMBINE
   unsigned long long rest = __ballot(esc);
   if (rest == 0ull) return;
+  if (!kCombine || !(fresh(L).wflags & kSplatCombine)) {  // (CVR_OPT_SAMPLE_ORDER 0: few shared pixels)
+    if (esc) splat(L, ps);
+    return;
+  }
   uint32_t leader = lane;
   bool multi = false;  // wave-uniform: some pixel gets two or more escapes
   while (rest != 0ull) {
@@ -241,12 +252,6 @@ __device__ __forceinline__ void splat_wave(Pool& S, const LaunchParams& L, const
     q.T = mk3(acc[0], acc[1], acc[2]);
     splat(L, q);
   }
-#else
-  (void)S;
-  (void)s;
-  (void)lane;
-  if (esc) splat(L, ps);
-#endif
 }
 
 // The wave's path cursor into the global work queues (as k_persistent).
@@ -273,16 +278,6 @@ __device__ __forceinline__ void record_end(const LaunchParams& L, uint32_t s, co
 }
 
 
-// The launch parameters as seen from code that runs rarely (the drain): the
-// LDS address goes through an empty asm each time, so the compiler cannot
-// hoist loads of L's fields out of the main loop and hold them in registers
-// across the track loop (the dense kernel has no VGPR to spare at 5 waves).
-typedef __attribute__((address_space(3))) const LaunchParams LdsParams;
-__device__ __forceinline__ const LaunchParams& fresh(const LaunchParams& L) {
-  LdsParams* p = (LdsParams*)&L;
-  asm volatile("" : "+v"(p));
-  return *(const LaunchParams*)p;
-}
 
 // ---- in-launch output (cvr_render_frame) -----------------------------------
 // getImage (CudaVolPath.cpp:339-347, ImageBufferTransfer.cu:61-78: Scale, then
@@ -905,7 +900,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         }
       }
       // the batch's escapes (camera rays that miss the box, survivors leaving it), per pixel
-      splat_wave(S, L, ps, escaped, s, lane);
+      // (the in-launch output instance splats per lane: combining cost it 2 VGPR spills)
+      splat_wave<!kFlush>(S, L, ps, escaped, s, lane);
       // a path's segments are the increments of its nseg (each counted once, as
       // the reference's per-iteration RAYS_STATISTICS count)
       {
@@ -948,7 +944,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       // The batch's new items then get no path and run no code; their slot
       // indices (the stack's stale entries) are never used.
       {
-        const uint32_t d = fresh(L).drain;
+        const uint32_t d = fresh(L).wflags & kDrainMask;
         n_ln = d ? 64u - min(64u, (n_live * d + d) / (d + 1u)) : 0u;
       }
     }
@@ -1018,7 +1014,7 @@ struct PairPool {
   uint32_t cnt[2][STAT_COUNT];
   unsigned long long dead[2];
   uint32_t cur[2][3];
-  uint32_t pad[2];
+  uint32_t gone[2];      // the wave has left its loop (every queue was found empty)
 };
 // events of list k (0 boundary, 1 collision) reserved and not yet claimed
 __device__ __forceinline__ uint32_t pair_avail(uint32_t heads, uint32_t tail, uint32_t k) {
@@ -1047,6 +1043,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
     L = Lk;
     S.tail[0] = S.tail[1] = 0u;
     S.heads = 0u;
+    S.gone[0] = S.gone[1] = 0u;
   }
   for (uint32_t i = threadIdx.x; i < 256u; i += 128u) {
     S.lb[i] = 0xFFu;
@@ -1092,14 +1089,32 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
     if (is_c) S.lc[(tc0 + lane_rank(mc)) & 255u] = (uint8_t)s;
   };
 
+  // Watchdog (the variant is an experiment): a wave that runs more outer iterations than
+  // any launch needs (C2: a wave runs ~10^3-10^4 batches) leaves its loop and reports
+  // it in the truncated counter (+2^20 per wave), so a scheduling bug ends the launch
+  // with wrong counters instead of hanging the GPU.
+  uint32_t watchdog = 0;
   for (;;) {
+    if (++watchdog > (1u << 22)) {
+      if (lane == 0) {
+        atomicAdd(&S.cnt[wv][STAT_TRUNCATED], 1u << 20);
+        __hip_atomic_store(&S.gone[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      break;
+    }
     __builtin_amdgcn_s_setprio(kPrioTrack);
     int slot = -1;
     int fst = 0;
     V3 o = mk3(0, 0, 0), d = mk3(0, 0, 0);
     Rng rng{0, 0, 0, 0, 0, 0};
     float t = 0.0f, max_t = 0.0f;
+    uint32_t tracks = 0;
     for (;;) {
+      if (++tracks > (1u << 24)) {  // (watchdog, as above: no segment takes this long)
+        if (lane == 0) atomicAdd(&S.cnt[wv][STAT_TRUNCATED], 1u << 20);
+        watchdog = 1u << 22;
+        break;
+      }
       const unsigned long long trk = (__ballot(slot >= 0) & __ballot(fst == 0));
       const uint32_t n_trk = (uint32_t)__popcll(trk);
       if (64u - n_trk >= batch || n_trk == 0u) {
@@ -1239,13 +1254,25 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
       hc = h >> 16;
     }
     const bool any_event = (tb | tc) != 0u;
-    // no path left: nothing to track, nothing shared, no new path to start
-    if (!any_event && n_ready == 0u && (n_ln == 0u || (S.cur[wv][2] & kCurExhausted))) {
+    if (!any_event && n_ready == 0u) {
       const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);
-      if (pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
-              pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1) ==
-          0u)
+      const bool shared_empty = pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
+                                    pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1) ==
+                                0u;
+      // no path left: nothing to track, nothing shared, no new path to start (or, holding no
+      // slot at all, the other wave has left: it did so only once every queue was empty)
+      if (shared_empty && ((S.cur[wv][2] & kCurExhausted) ||
+                           (n_ln == 0u && __hip_atomic_load(&S.gone[wv ^ 1u], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP) != 0u))) {
+        if (lane == 0) __hip_atomic_store(&S.gone[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
+      }
+      // the other wave holds every slot (this wave has none free and none ready): wait for
+      // it to file events this wave can take, without taking its issue slots meanwhile
+      if (n_ln == 0u) {
+        __builtin_amdgcn_s_sleep(4);
+        continue;
+      }
     }
     MediumParams me = m;
     me.g = opaque_s(m.g);
@@ -1390,7 +1417,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
           }
         }
       }
-      splat_wave(S, L, ps, escaped, s, lane);
+      splat_wave<true>(S, L, ps, escaped, s, lane);
       {
         const uint32_t n_seg = (uint32_t)(__popcll(__ballot(seg_first)) + __popcll(__ballot(seg_next)));
         const uint32_t n_esc = (uint32_t)__popcll(__ballot(escaped)), n_tr = (uint32_t)__popcll(__ballot(truncated));
@@ -1412,7 +1439,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
       const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);
       const uint32_t n_live = n_ready + pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
                               pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1);
-      const uint32_t dr = fresh(L).drain;
+      const uint32_t dr = fresh(L).wflags & kDrainMask;
       n_ln = dr ? 64u - min(64u, (n_live * dr + dr) / (dr + 1u)) : 0u;
     }
   }

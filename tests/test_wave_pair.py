@@ -50,6 +50,7 @@ def test_pair_vs_oracle_and_block_shards(cvr, oracle_mod):
     scene = cvr.Scene.synthetic("manix")
     W, H, iters = 128, 128, 3
     c, iv, r2v = _ctx(cvr, scene, W, H, "regenerationSK", 1)
+    c.set_seed(0)
     img, st = c.render_image(W, H, (1, 1), iters)
     orc = oracle_for_scene(oracle_mod, scene)
     ref, rst = oracle_image(orc, iv, r2v, W, H, (1, 1), iters, 2)
@@ -59,6 +60,7 @@ def test_pair_vs_oracle_and_block_shards(cvr, oracle_mod):
     acc = np.zeros_like(img)
     for r in range(3):
         c.set_block_shard(r, 3)
+        c.set_seed(0)  # render_image advances the seed as reset() does
         part, _ = c.render_image(W, H, (1, 1), iters)
         acc += np.where(np.isnan(part), 0, part)
     c.close()

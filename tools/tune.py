@@ -100,6 +100,8 @@ def main():
             c.set_option(cvr.OPT_POOL, d["pool"])
         if "pair" in d:
             c.set_option(cvr.OPT_WAVE_PAIR, d["pair"])
+        if "sorder" in d:
+            c.set_option(cvr.OPT_SAMPLE_ORDER, d["sorder"])
         c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
         c.init()
         c.set_resolution(W, H)
