@@ -142,7 +142,7 @@ struct cvr_ctx {
   int wpool_waves = 0;
   int morton = 0;  // CVR_OPT_MORTON
   int wave_pair = 0;  // CVR_OPT_WAVE_PAIR
-  int sample_order = 0;  // CVR_OPT_SAMPLE_ORDER
+  int sample_order = -1;  // CVR_OPT_SAMPLE_ORDER (-1: 1 for a sparse medium, else 0)
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
@@ -1209,7 +1209,7 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       c->use_cells = v != 0;
       return CVR_OK;
     case CVR_OPT_SAMPLE_ORDER:
-      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "sample order must be 0 or 1");
+      if (v < -1 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "sample order must be -1, 0 or 1");
       c->sample_order = (int)v;
       return CVR_OK;
     case CVR_OPT_WAVE_PAIR:
@@ -1323,7 +1323,10 @@ int cvr_launch_render(cvr_ctx* c) {
   }
   if (scheduler_for(c) == 3) {
     L.wflags = (uint32_t)(c->drain < 0 ? 1 : c->drain) & cvr::kDrainMask;
-    if (c->sample_order == 1) L.wflags |= cvr::kUnitSampleInner | cvr::kSplatCombine;
+    // samples innermost + combined splats: C5 -1.4% (123.0 vs 124.7 ms), dense C2 / C3 +2.7% /
+    // +3.6% (profiles/round5/ab/call6_sample_order_ab.log, call7): on by default for sparse media
+    const int so = c->sample_order >= 0 ? c->sample_order : (c->m.leaves != nullptr ? 1 : 0);
+    if (so == 1) L.wflags |= cvr::kUnitSampleInner | cvr::kSplatCombine;
   }
   // The persistent schedulers' u32 queue heads run past a queue's end by at
   // most one chunk per wave before every wave sees the queue exhausted

@@ -1073,7 +1073,10 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
   // File lanes' slots into the shared lists: mb boundary, mc collision lanes.
   // The slot's LDS state is written before: the release fence orders it (and
   // the wave's pool_T stores) before the list entries the other wave may read.
-  auto file_shared = [&](bool is_b, bool is_c, uint32_t s) {
+  // full: the entries follow global pool_T stores of this batch (vmcnt wait); from the
+  // track loop only LDS state precedes them, and one wave's LDS operations are performed in
+  // order, so a compiler barrier suffices.
+  auto file_shared = [&](bool is_b, bool is_c, uint32_t s, bool full) {
     const unsigned long long mb = __ballot(is_b), mc = __ballot(is_c);
     const uint32_t kb = (uint32_t)__popcll(mb), kc = (uint32_t)__popcll(mc);
     if ((kb | kc) == 0u) return;
@@ -1084,9 +1087,20 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
     }
     tb0 = __builtin_amdgcn_readfirstlane(tb0);
     tc0 = __builtin_amdgcn_readfirstlane(tc0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (is_b) S.lb[(tb0 + lane_rank(mb)) & 255u] = (uint8_t)s;
-    if (is_c) S.lc[(tc0 + lane_rank(mc)) & 255u] = (uint8_t)s;
+    if (full) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    else __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    // An entry is written only once the taker of the same ring position one lap earlier
+    // has read it (it writes 0xFF back): a taker that claimed its entries but was kept from
+    // reading them (its wave starved at a lower priority while the rings went round) would
+    // otherwise read a later lap's entry and leave the later taker waiting for ever.
+    if (is_b || is_c) {
+      uint8_t* e = is_b ? &S.lb[(tb0 + lane_rank(mb)) & 255u] : &S.lc[(tc0 + lane_rank(mc)) & 255u];
+      uint32_t spins = 0;
+      while (__hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0xFFu && ++spins < (1u << 16)) {
+      }
+      if (spins >= (1u << 16)) atomicAdd(&S.cnt[wv][STAT_TRUNCATED], 1u);  // (bug report, as below)
+      __hip_atomic_store(e, (uint8_t)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   };
 
   // Watchdog (the variant is an experiment): a wave that runs more outer iterations than
@@ -1094,6 +1108,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
   // it in the truncated counter (+2^20 per wave), so a scheduling bug ends the launch
   // with wrong counters instead of hanging the GPU.
   uint32_t watchdog = 0;
+  uint32_t n_mine = 0;  // events this wave filed since its last batch (its batch trigger)
   for (;;) {
     if (++watchdog > (1u << 22)) {
       if (lane == 0) {
@@ -1121,7 +1136,8 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
         if (fst == 2 && !(t < max_t)) fst = 3;
         if (fst != 0) store_track(S, (uint32_t)slot, t, rng);
         n_over += (uint32_t)__popcll(__ballot(fst == 1));
-        file_shared((fst & 1) != 0, fst == 2, (uint32_t)slot);
+        n_mine += (uint32_t)__popcll(__ballot(fst != 0));
+        file_shared((fst & 1) != 0, fst == 2, (uint32_t)slot, false);
         if (fst != 0) {
           slot = -1;
           fst = 0;
@@ -1140,17 +1156,16 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
       }
       const uint32_t n_act = (uint32_t)__popcll((__ballot(slot >= 0) & __ballot(fst == 0)));
       const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0));
-      const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);
-      const uint32_t n_shared = pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
-                                pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1);
-      if (n_shared + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
+      // the trigger counts this wave's own filings since its last batch (registers only, as
+      // k_wpool); the batch then takes what both waves have filed
+      if (n_mine + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
         if (fst == 2 && !(t < max_t)) fst = 3;
         if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
         const unsigned long long mr = (__ballot(slot >= 0) & __ballot(fst == 0));
         if (slot >= 0 && fst == 0) S.ready[wv][(ready_head + n_ready + lane_rank(mr)) % kN] = (uint8_t)slot;
         n_over += (uint32_t)__popcll(__ballot(fst == 1));
         n_ready += (uint32_t)__popcll(mr);
-        file_shared((fst & 1) != 0, fst == 2, (uint32_t)slot);
+        file_shared((fst & 1) != 0, fst == 2, (uint32_t)slot, false);
         break;
       }
 #pragma unroll
@@ -1220,8 +1235,9 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
         }
       }
     }
-    // claim the batch's events from the shared lists (kind-major thresholds as k_wpool)
-    __builtin_amdgcn_s_setprio(kPrioEvent);
+    // claim the batch's events from the shared lists (kind-major thresholds as k_wpool), at
+    // the top priority until they are read (see file_shared)
+    __builtin_amdgcn_s_setprio(3);
     uint32_t tb = 0, tc = 0, hb = 0, hc = 0;
     {
       uint32_t h = __builtin_amdgcn_readfirstlane(S.heads);
@@ -1259,13 +1275,18 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
       const bool shared_empty = pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[0]), 0) +
                                     pair_avail(hs, __builtin_amdgcn_readfirstlane(S.tail[1]), 1) ==
                                 0u;
-      // no path left: nothing to track, nothing shared, no new path to start (or, holding no
-      // slot at all, the other wave has left: it did so only once every queue was empty)
-      if (shared_empty && ((S.cur[wv][2] & kCurExhausted) ||
-                           (n_ln == 0u && __hip_atomic_load(&S.gone[wv ^ 1u], __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP) != 0u))) {
+      // no path left: nothing to track, nothing shared, no new path to start
+      if (shared_empty && (S.cur[wv][2] & kCurExhausted)) {
         if (lane == 0) __hip_atomic_store(&S.gone[wv], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         break;
+      }
+      // holding no slot at all while the other wave has left (with every slot free): this
+      // wave takes all of them and goes on with its queue cursor
+      if (shared_empty && n_ln == 0u &&
+          __hip_atomic_load(&S.gone[wv ^ 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u) {
+        for (uint32_t i = lane; i < (uint32_t)kN; i += 64u) S.ln[wv][i] = (uint8_t)i;
+        n_ln = kN;
+        continue;
       }
       // the other wave holds every slot (this wave has none free and none ready): wait for
       // it to file events this wave can take, without taking its issue slots meanwhile
@@ -1295,7 +1316,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
         uint32_t v, spins = 0;
         do {
           v = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } while (v == 0xFFu && ++spins < (1u << 24));
+        } while (v == 0xFFu && ++spins < (1u << 16));
         // (a bounded wait: an entry that never appears would be a bug; the item is then
         // dropped and counted as truncated, so the launch ends and the counters differ)
         __hip_atomic_store(q, (uint8_t)0xFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1307,6 +1328,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
         s = S.ln[wv][n_ln - 1u - (lane - tb - tc)];
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the filer's slot state and pool_T stores
+      __builtin_amdgcn_s_setprio(kPrioEvent);
       n_ln -= tn;
       PathState ps{};
       Isect is{};
@@ -1433,7 +1455,8 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
       if (to_ln) S.ln[wv][n_ln + lane_rank(mn)] = (uint8_t)s;
       n_ready += (uint32_t)__popcll(mr);
       n_ln += (uint32_t)__popcll(mn);
-      file_shared(to_lb, false, s);
+      n_mine = (uint32_t)__popcll(__ballot(to_lb));
+      file_shared(to_lb, false, s, true);
     }
     if (S.cur[wv][2] & kCurExhausted) {
       const uint32_t hs = __builtin_amdgcn_readfirstlane(S.heads);

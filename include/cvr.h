@@ -142,12 +142,13 @@ typedef enum {
                                  ended (cvr_frame_flush_info); 0 normalise + copy after the launch.
                                  Same image either way (C2: 5.14 vs 5.29 ms per call).  2 (tests):
                                  the flushers give up at once, so the call takes its fallback copy. */
-  CVR_OPT_SAMPLE_ORDER = 27,   /* wave-pool scheduler, pixel-block work order: 0 (default) within an 8x8
-                                 block the units run sample by sample, the 64 pixels innermost; 1 pixel
-                                 by pixel with the samples innermost, and each event batch sums its
-                                 escapes per pixel before the framebuffer atomics (C3: 2.23 -> 0.99 GB
-                                 written per launch; kernel ~1% slower on C2; the
-                                 in-launch output of cvr_render_frame keeps per-lane atomics).
+  CVR_OPT_SAMPLE_ORDER = 27,   /* wave-pool scheduler, pixel-block work order: 0 within an 8x8 block the
+                                 units run sample by sample, the 64 pixels innermost; 1 pixel by pixel
+                                 with the samples innermost, and each event batch sums its escapes per
+                                 pixel before the framebuffer atomics (C3: 2.23 -> 0.99 GB written per
+                                 launch; the in-launch output of cvr_render_frame keeps per-lane
+                                 atomics).  -1 (default): 1 for a sparse medium (C5 -1.4%), 0 for a
+                                 dense one (C2 / C3 +2.7% / +3.6% with 1).
                                  Scheduling and summation order only. */
   CVR_OPT_WAVE_PAIR = 26,      /* wave-pool scheduler, dense media with cells and bounds: 1 runs two waves
                                  per workgroup whose boundary and collision event lists are shared

@@ -57,6 +57,8 @@ for step in "$@"; do
     tunev:*) IFS=: read -r _ sc rounds vs <<< "$step"; run tunev_$sc 400 python3 tools/tune.py --scene $sc --rounds $rounds --variants ${vs//;/ } ;;
     # selected GPU test files: pytestf:tests/a.py,tests/b.py
     pytestf:*) fs=${step#pytestf:}; run pytestf 900 python3 -u -m pytest ${fs//,/ } -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider ;;
+    # the same at a resolution: tunevr:SCENE:RES:ROUNDS:variant;variant
+    tunevr:*) IFS=: read -r _ sc res rounds vs <<< "$step"; run tunevr_${sc}_$res 400 python3 tools/tune.py --scene $sc --res $res --rounds $rounds --variants ${vs//;/ } ;;
     # the driver's default bench line
     benchdef) run benchdef 600 python3 bench.py ;;
     # arbitrary counters on a scene's bench run: pmcx:SCENE:CTR1,CTR2,...

@@ -15,7 +15,7 @@ for d in sorted(glob.glob(os.path.join(root, "*"))):
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if "k_wpool" not in r["Kernel_Name"]:
+            if "k_wpool" not in r["Kernel_Name"] and "k_wpair" not in r["Kernel_Name"]:
                 continue
             k = (r["Counter_Name"], int(r["Dispatch_Id"]))
             vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
@@ -32,4 +32,8 @@ for d in sorted(glob.glob(os.path.join(root, "*"))):
             out.append(f"{ctr} {v:.3f} GB")
         else:
             out.append(f"{ctr} {v:.4g}")
+    vals2 = {c: sum(vals[(c, i)] for i in sorted(i for cc, i in vals if cc == c)[1:] or
+                    sorted(i for cc, i in vals if cc == c)) for c in {c for c, _ in vals}}
+    if "SQ_INSTS_VALU" in vals2 and "SQ_THREAD_CYCLES_VALU" in vals2:
+        out.append(f"lanes/VALU {vals2['SQ_THREAD_CYCLES_VALU'] / vals2['SQ_INSTS_VALU']:.2f}")
     print(os.path.basename(d), " | ".join(out))

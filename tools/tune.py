@@ -113,6 +113,7 @@ def main():
     times = {v: [] for v, _ in ctxs}
     extra = {}
     for r in range(a.rounds + 1):
+        print(f"round {r}/{a.rounds}", file=sys.stderr, flush=True)  # (progress: long runs stay observable)
         for v, c in ctxs:
             c.clear_output()
             t0 = time.perf_counter()
