@@ -1325,7 +1325,12 @@ int cvr_launch_render(cvr_ctx* c) {
     L.wflags = (uint32_t)(c->drain < 0 ? 1 : c->drain) & cvr::kDrainMask;
     // samples innermost + combined splats: C5 -1.4% (123.0 vs 124.7 ms), dense C2 / C3 +2.7% /
     // +3.6% (profiles/round5/ab/call6_sample_order_ab.log, call7): on by default for sparse media
-    const int so = c->sample_order >= 0 ? c->sample_order : (c->m.leaves != nullptr ? 1 : 0);
+    // The in-launch output instance (cvr_render_frame) splats per lane (combining cost its
+    // dense instance two VGPR spills), and per-lane splats with samples innermost put the same
+    // pixel on several lanes of one atomic instruction, which the memory side serialises (C5 one
+    // render 2086 vs 2666 Msamples/s): that launch keeps the sample-major order.
+    int so = c->sample_order >= 0 ? c->sample_order : (c->m.leaves != nullptr ? 1 : 0);
+    if (c->frame_done_active) so = 0;
     if (so == 1) L.wflags |= cvr::kUnitSampleInner | cvr::kSplatCombine;
   }
   // The persistent schedulers' u32 queue heads run past a queue's end by at

@@ -146,8 +146,8 @@ typedef enum {
                                  units run sample by sample, the 64 pixels innermost; 1 pixel by pixel
                                  with the samples innermost, and each event batch sums its escapes per
                                  pixel before the framebuffer atomics (C3: 2.23 -> 0.99 GB written per
-                                 launch; the in-launch output of cvr_render_frame keeps per-lane
-                                 atomics).  -1 (default): 1 for a sparse medium (C5 -1.4%), 0 for a
+                                 launch; a launch with cvr_render_frame's in-launch output keeps
+                                 order 0 and per-lane atomics).  -1 (default): 1 for a sparse medium (C5 -1.4%), 0 for a
                                  dense one (C2 / C3 +2.7% / +3.6% with 1).
                                  Scheduling and summation order only. */
   CVR_OPT_WAVE_PAIR = 26,      /* wave-pool scheduler, dense media with cells and bounds: 1 runs two waves

@@ -16,9 +16,12 @@ for sc in manix hetvol cloud; do
   if [ $sc = cloud ]; then sw="3 1"; else sw="20 5"; fi
   python3 tools/kernel_phases.py $F/prof_$sc/run_kernel_trace.csv "$inst" $sw $P/${c}_kernel_phases.json $F/prof_$sc.log | grep "_ms\|_over_"
 done
-python3 tools/pmc_summary.py $P/pmc_k_wpool.json k_wpool $F/pmc_a $F/pmc_b $F/pmc_c $F/pmc_d
-python3 tools/pmc_summary.py $P/pmc_k_wpool_cloud.json k_wpool $F/pmc5_a $F/pmc5_b $F/pmc5_c
+if [ -d $F/pmc_d ]; then  # final_profile.sh part 2
+  python3 tools/pmc_summary.py $P/pmc_k_wpool.json k_wpool $F/pmc_a $F/pmc_b $F/pmc_c $F/pmc_d
+  python3 tools/pmc_summary.py $P/pmc_k_wpool_cloud.json k_wpool $F/pmc5_a $F/pmc5_b $F/pmc5_c
+fi
 for c in c1 c2 c3 c4 c5; do
+  [ -f $F/${c}_bench.log ] || continue
   cp $F/${c}_bench.log $P/${c}_bench.log
   grep '^{' $F/${c}_bench.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; cb=d.get('cpu_baseline') or {}
@@ -26,4 +29,5 @@ print('$c value', d['value'], 'ms', d['ms_per_step'], 'kernel', r['kernel_ms'], 
       'serial', d.get('serial',{}).get('value'), 'cpu', cb.get('value'), 'traffic', r['traffic'], 'hbm_frac', r['hbm_frac_measured'])"
 done
 cp $F/pytest_gpu.log $P/pytest_gpu.log; cp $F/smoke.log $P/smoke.log; cp $F/libcvr.sha256 $P/libcvr.sha256
+for f in $F/k_*.log $F/pair_*.log; do [ -f "$f" ] && cp "$f" $P/; done
 tail -1 $P/pytest_gpu.log; tail -1 $P/smoke.log; cat $P/libcvr.sha256; sha256sum cudavolumerenderer_amd/libcvr.so

@@ -19,6 +19,8 @@ step() {  # name seconds cmd...
   [ $rc -eq 0 ] || { tail -20 "$OUT/$name.log"; exit $rc; }
 }
 B="python3 bench.py --no-cpu-baseline"
+PART=${1:-all}  # 1: tests, traces, traffic / VALU passes, bench lines; 2: SQ groups, kernel ids, pair
+if [ "$PART" != 2 ]; then
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 600 python3 -u -m pytest tests -m gpu -q --timeout 300 -p no:cacheprovider
 for sc in manix hetvol cloud; do
@@ -47,6 +49,8 @@ step c1_bench 200 python3 bench.py --scene bucky --steps 20 --warmup 5
 step c3_bench 200 python3 bench.py --scene hetvol --steps 20 --warmup 5
 step c5_bench 400 python3 bench.py --scene cloud --steps 5 --warmup 1
 step c4_bench 400 $B --shard tiles --resolution 2048 2048 --iterations 256 --steps 2 --warmup 1
+fi
+[ "$PART" = 1 ] && { echo "final profile part 1 done"; exit 0; }
 step pmc_a 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc_a" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
 step pmc_b 200 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc_b" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
 step pmc_c 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc_c" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
@@ -55,4 +59,11 @@ C5="$B --scene cloud --serial --steps 2 --warmup 1"
 step pmc5_a 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc5_a" -o run --output-format csv -- $C5
 step pmc5_b 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc5_b" -o run --output-format csv -- $C5
 step pmc5_c 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc5_c" -o run --output-format csv -- $C5
+# round 5: every kernel id's C2 line (all on the wave pool by default), and the paired-wave
+# variant (CVR_OPT_WAVE_PAIR) against the one-wave pool with the lane-fill counters
+for k in streamingSK sortingSK streamingMK naiveSK naiveMK; do
+  step k_$k 300 python3 bench.py --kernel $k --steps 20 --warmup 5 --no-shard-emulation --no-cpu-baseline
+done
+step pair_pmc 400 bash tools/pmc_tune.sh "SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" manix,hetvol one=regenerationSK: pair=regenerationSK:pair=1
+step pair_time 300 python3 tools/tune.py --scene manix --rounds 4 --variants regenerationSK: regenerationSK:pair=1
 echo "final profile done"
