@@ -244,6 +244,15 @@ int wpool_waves_for(const cvr_ctx* c, bool sparse) {
   return 5;  // dense and sparse (split slots: DESIGN.md §6)
 }
 
+// naiveMK runs the wave pool (k_wpool's kMedMK instances: d_init + d_extend per path, RNG
+// re-seeded per bounce; C2 27.5 -> ~4.5 ms) unless another scheduler or budget is asked
+// for, the reference's per-bounce compaction (CVR_OPT_MK_COMPACTION 1) or the in-launch
+// output (cvr_render_frame then copies after the launch).
+bool mk_on_wpool(const cvr_ctx* c) {
+  return c->kernel == CVR_KERNEL_NAIVE_MK && scheduler_for(c) == 3 && !c->mk_compaction &&
+         wpool_waves_for(c, c->m.leaves != nullptr) == 5;
+}
+
 // Wave-pool grid of a launch of n_paths (one wave per workgroup): CVR_OPT_GRID,
 // else the occupancy grid, of which a small launch takes a part.  A launch of
 // fewer than 64 paths per wave (C1: 262 K paths) ends mostly in ramp-up and
@@ -304,7 +313,8 @@ void fill_launch(const cvr_ctx* c, cvr::LaunchParams& L, uint64_t first, uint64_
   const uint64_t P0 = (uint64_t)(uint32_t)((float)c->tile_w * (float)c->tile_h);
   // the persistent schedulers take work units through unit_to_path (pixel-block order); naiveSK/MK
   // and the wavefront pair map launch index -> path id directly
-  const bool queued = c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 && scheduler_for(c) != kSchedPerItem &&
+  const bool queued = (c->kernel != CVR_KERNEL_NAIVE_MK || mk_on_wpool(c)) && scheduler_for(c) != 1 &&
+                      scheduler_for(c) != kSchedPerItem &&
                       c->rng_binding == 0;
   const bool block_order = queued && c->order && P0 && first % P0 == 0 && count % P0 == 0 && count > 0 &&
                            count / P0 <= (1ull << 20) && c->tile_w % 8 == 0 && c->tile_h % 8 == 0;
@@ -1375,7 +1385,7 @@ int cvr_launch_render(cvr_ctx* c) {
     }
   } else if (c->kernel == CVR_KERNEL_NAIVE_MK && c->mk_compaction) {
     if ((r = mk_reference_render(c, L))) return r;
-  } else if (c->kernel == CVR_KERNEL_NAIVE_MK) {
+  } else if (c->kernel == CVR_KERNEL_NAIVE_MK && !mk_on_wpool(c)) {
     HIP_TRY(c, cvr::launch_naive_mk(launch_medium(c), L, c->stream));
   } else if (scheduler_for(c) == kSchedPerItem) {
     HIP_TRY(c, cvr::launch_naive(launch_medium(c), L, eps, c->stream));
@@ -1406,7 +1416,8 @@ int cvr_launch_render(cvr_ctx* c) {
                        4 * cvr::kFrameFlushers);
       L.frame_done = c->frame_done_active;
     }
-    HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream, c->wave_pair != 0));
+    HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream, c->wave_pair != 0,
+                                 c->kernel == CVR_KERNEL_NAIVE_MK));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }
@@ -1883,7 +1894,8 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, size_t host_floats, uint32_t
   compute_range(c, &first, &count);
   cvr::LaunchParams L0{};
   fill_launch(c, L0, first, count);
-  const bool queued = c->kernel != CVR_KERNEL_NAIVE_MK && scheduler_for(c) != 1 && scheduler_for(c) != kSchedPerItem &&
+  const bool queued = (c->kernel != CVR_KERNEL_NAIVE_MK || mk_on_wpool(c)) && scheduler_for(c) != 1 &&
+                      scheduler_for(c) != kSchedPerItem &&
                       c->rng_binding == 0;
   const uint32_t brows = (L0.order == 1 && queued && c->shard_world == 1) ? H / 8u : 0u;
   if (parts == 0) parts = 1;
@@ -1904,6 +1916,7 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, size_t host_floats, uint32_t
   // the GPU can store into
   void* dhost = nullptr;
   if (c->frame_flush && parts == 1 && brows && scheduler_for(c) == 3 && !c->d_rec_active &&
+      c->kernel != CVR_KERNEL_NAIVE_MK &&  // (no in-launch output instance of naiveMK's walk)
       wpool_waves_for(c, c->m.leaves != nullptr) == 5 && wpool_launch_grid(c, L0.path_count) > 4 * cvr::kFrameFlushers) {
     if (hipHostGetDevicePointer(&dhost, host_image, 0) != hipSuccess) {
       (void)hipGetLastError();  // pageable memory: not an error, the copy path below

@@ -53,9 +53,10 @@ hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatt
 hipError_t launch_pool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid, hipStream_t s);
 hipError_t pool_occupancy(bool scatter_eps, int* blocks_per_cu);
 // pair: two waves per workgroup sharing their event lists (k_wpair; dense media with
-// cells and bounds, 5 waves per SIMD, no records / in-launch output; else k_wpool)
+// cells and bounds, 5 waves per SIMD, no records / in-launch output; else k_wpool).
+// naive_mk: naiveMK's walk on the wave pool (5 waves per SIMD, no records / in-launch output).
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
-                        hipStream_t s, bool pair = false);
+                        hipStream_t s, bool pair = false, bool naive_mk = false);
 hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu);
 // Pool slots per wave of the wave-pool kernel instance (LaunchParams::pool_T
 // needs grid * slots float4).

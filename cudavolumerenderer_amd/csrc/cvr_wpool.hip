@@ -129,13 +129,14 @@ __device__ __forceinline__ V3 normal_of(uint32_t c) {
 
 template <class Pool>
 __device__ __forceinline__ void store_full(Pool& S, float4* __restrict__ gT, uint32_t s,
-                                           const PathState& ps, const Isect& is, uint32_t nseg) {
+                                           const PathState& ps, const Isect& is, uint32_t nseg,
+                                           uint32_t wword) {
   S.a[s] = make_float4(ps.o.x, ps.o.y, ps.o.z, 0.0f);
   S.b[s] = make_float4(ps.d.x, ps.d.y, ps.d.z, is.dist);
   S.c[s] = make_uint4(ps.rng.v0, ps.rng.v1, ps.rng.v2, ps.rng.v3);
   S.e[s] = make_uint2(ps.rng.v4, ps.rng.d);
   S.meta[s] = normal_code(is.normal) | (is.inside ? 8u : 0u) | (nseg << 4);
-  gstore4(gT + s, make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(ps.image_id)));
+  gstore4(gT + s, make_float4(ps.T.x, ps.T.y, ps.T.z, __uint_as_float(wword)));
 }
 template <class Pool>
 __device__ __forceinline__ void load_full(const Pool& S, const float4* __restrict__ gT, uint32_t s,
@@ -441,8 +442,17 @@ __device__ void frame_flusher(const LaunchParams& L) {
 // kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
 // the other instances carry none of its code.
 enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2, kMedDenseFullUniform = 3 };
-template <bool kScatterEps, int kWaves, int kMed, bool kRecord, bool kFlush>
+// kMedMK (or-ed into kMed): naiveMK's walk (NaiveVolPTmk_kernel.cuh:20-151) on the wave
+// pool, round 5: a new path runs d_init (camera ray on the (iteration, pixel, 0) stream,
+// AABB, the GGX sample at the box, Q12) and every segment starts as d_extend does, with
+// the RNG re-seeded from (iteration, pixel, depth) and three unused draws; the slot's
+// event-only word holds the path id (iteration and pixel) instead of the pixel.
+constexpr int kMedMK = 4;
+template <bool kScatterEps, int kWaves, int kMedMk, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
+  constexpr bool kMK = (kMedMk & kMedMK) != 0;
+  constexpr int kMed = kMedMk & 3;
+  static_assert(!kMK || (kScatterEps && !kRecord && !kFlush), "naiveMK: scatter -eps, no records / in-launch output");
   constexpr bool kSparse = kMed == kMedSparse;
   // Sparse media defer their cell fetches to the end of the track iteration
   // (the lookahead below): C5 -3.0%; the dense instances lose 5-8% with it.
@@ -770,8 +780,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       PathState ps{};
       Isect is{};
       uint32_t nseg = 0;
+      uint32_t mk_pid = 0;  // naiveMK: the path id (its iteration and pixel seed every segment)
       float t_hit = 0.0f;
       bool to_ready = false, to_lb = false, to_ln = false;
+      bool alive = false;
       bool truncated = false, escaped = false, seg_first = false, seg_next = false;  // counted by ballots
       // ---- regeneration (new items): the wave's cursor into the global queues
       const unsigned long long want = __ballot(kind == K_NEW);
@@ -817,7 +829,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           const uint32_t take = min((uint32_t)__popcll(want) - given, cend - cnext);
           if (kind == K_NEW && rank >= given && rank < given + take) {
             const uint32_t pid = unit_to_path(L, cqh & 0xFFu, cnext + (rank - given));
-            path_begin(L, pid, ps);
+            if constexpr (kMK) {
+              mk_pid = pid;
+            } else {
+              path_begin(L, pid, ps);
+            }
             if (kRecord) rec_pids<kSlots>(L)[s] = pid;
             is.normal = mk3(0, 0, 0);
             nseg = 0;
@@ -835,7 +851,24 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         // that got no path (queues exhausted) files its slot as free again
         const uint32_t n_got = (uint32_t)__popcll(__ballot(got));
         if (lane == 0) S.cnt[STAT_PATHS] += n_got;
-        if (got) {
+        if constexpr (kMK) {
+          // d_init (NaiveVolPTmk_kernel.cuh:20-77, mk_init): a miss adds (1,1,1), a failed
+          // GGX sample drops the path, else its first d_extend starts below (alive)
+          if (got) {
+            const uint32_t it = fastdiv(mk_pid, L.div_tile_px);
+            nseg = 1;
+            seg_first = true;
+            const uint32_t r0 = mk_init(me, L, it, mk_pid - it * L.tile_px, ps);
+            if (r0 == MK_MISSED) {
+              escaped = true;
+              to_ln = true;
+            } else if (r0 == MK_DROPPED) {
+              to_ln = true;
+            } else {
+              alive = true;
+            }
+          }
+        } else if (got) {
           if (L.max_segments && nseg >= L.max_segments) {
             truncated = true;
             to_ln = true;
@@ -850,7 +883,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
               if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
               if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
             } else if (is.inside) {
-              store_full(S, L.pool_T + (size_t)blockIdx.x * kSlots, s, ps, is, nseg);
+              store_full(S, L.pool_T + (size_t)blockIdx.x * kSlots, s, ps, is, nseg, ps.image_id);
               to_ready = true;
             } else {
               kind = K_BOUNDARY;  // enters the box: boundary event in this batch
@@ -859,10 +892,15 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         }
       }
       float4* __restrict__ gT = L.pool_T + (size_t)blockIdx.x * kSlots;  // this wave's event-only slot part
-      if (lane < tb + tc) load_full(S, gT, s, ps, is, nseg, t_hit);
+      if (lane < tb + tc) {
+        load_full(S, gT, s, ps, is, nseg, t_hit);
+        if constexpr (kMK) {  // the event-only word is the path id
+          mk_pid = ps.image_id;
+          ps.image_id = mk_pid - fastdiv(mk_pid, L.div_tile_px) * L.tile_px;
+        }
+      }
       // a filed boundary whose last step passed max_t drew one number too many
       if (lane < tb && !(t_hit <= is.dist)) rng_undo(ps.rng);
-      bool alive = false;
       if (kind == K_BOUNDARY) {
         boundary_event(me, ps, is);
         alive = roulette(ps);
@@ -887,13 +925,25 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
         } else {
           ++nseg;
           seg_next = true;
+          if constexpr (kMK) {
+            // d_extend(depth) (NaiveVolPTmk_kernel.cuh:79-151): re-seed from (iteration,
+            // pixel, depth), three unused draws (Q12), a fresh SimpleIsect
+            const uint32_t it = fastdiv(mk_pid, L.div_tile_px);
+            rng_seeded(ps.rng, it, ps.image_id, nseg - 2u);
+            (void)rng_float(ps.rng);
+            (void)rng_float(ps.rng);
+            (void)rng_float(ps.rng);
+            is.dist = 0.0f;
+            is.normal = mk3(0, 0, 0);
+            is.inside = false;
+          }
           if (!aabb_intersect(me, ps.o, ps.d, is)) {
             escaped = true;  // splat below (splat_wave)
             to_ln = true;
             if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
             if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
           } else {
-            store_full(S, gT, s, ps, is, nseg);
+            store_full(S, gT, s, ps, is, nseg, kMK ? mk_pid : ps.image_id);
             to_ready = is.inside;  // medium: Woodcock from t = 0
             to_lb = !is.inside;    // no medium: boundary at isect.dist
           }
@@ -1400,7 +1450,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
               escaped = true;
               to_ln = true;
             } else if (is.inside) {
-              store_full(S, gT, s, ps, is, nseg);
+              store_full(S, gT, s, ps, is, nseg, ps.image_id);
               to_ready = true;
             } else {
               kind = K_BOUNDARY;
@@ -1433,7 +1483,7 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
             escaped = true;
             to_ln = true;
           } else {
-            store_full(S, gT, s, ps, is, nseg);
+            store_full(S, gT, s, ps, is, nseg, ps.image_id);
             to_ready = is.inside;
             to_lb = !is.inside;
           }
@@ -1509,14 +1559,31 @@ static const void* wpool_record_fn(int waves, bool sparse) {
   return waves == 5 ? reinterpret_cast<const void*>(&k_wpool<E, 5, kMedDense, true, false>) : nullptr;
 }
 
+// naiveMK instances (kMedMK): 5 waves per SIMD, every medium layout, scatter -eps.
+static const void* wpool_mk_fn(bool sparse, bool full, bool uniform) {
+#define CVR_WPMK(M) reinterpret_cast<const void*>(&k_wpool<true, 5, (M) | kMedMK, false, false>)
+  if (sparse) return CVR_WPMK(kMedSparse);
+  if (full && uniform) return CVR_WPMK(kMedDenseFullUniform);
+  if (full) return CVR_WPMK(kMedDenseFull);
+  return CVR_WPMK(kMedDense);
+#undef CVR_WPMK
+}
+
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
-                        hipStream_t s, bool pair) {
+                        hipStream_t s, bool pair, bool naive_mk) {
   if (L.path_count == 0) return hipSuccess;
   const bool sparse = m.leaves != nullptr;
   const bool flush = L.frame_done != nullptr;
   const bool full = !sparse && m.cells != nullptr && m.bounds != nullptr;
   const bool uniform = m.albedo_uniform != 0u;
   if (L.rec && flush) return hipErrorInvalidValue;
+  if (naive_mk) {
+    if (waves != 5 || flush || L.rec) return hipErrorInvalidValue;
+    MediumParams mm = m;
+    LaunchParams ll = L;
+    void* args[] = {&mm, &ll};
+    return hipLaunchKernel(wpool_mk_fn(sparse, full, uniform), dim3(grid), dim3(64), args, 0, s);
+  }
   if (pair && waves == 5 && full && !flush && !L.rec && grid >= 2) {
     // paired waves (workgroup-shared event lists): two waves per workgroup
 #define CVR_WPAIR(E, M) reinterpret_cast<const void*>(&k_wpair<E, 5, M>)
