@@ -30,7 +30,7 @@ OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1,
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
 OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT, OPT_FRAME_FLUSH = 18, 19, 20, 22, 23, 24
-OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR, OPT_SAMPLE_ORDER = 25, 26, 27
+OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR, OPT_SAMPLE_ORDER, OPT_EMPTY_MASK = 25, 26, 27, 28
 
 
 class CvrError(RuntimeError):

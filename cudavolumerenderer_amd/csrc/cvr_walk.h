@@ -173,7 +173,19 @@ struct MediumParams {
   // loaded (the same values, so the same result).  Last, so that the other fields
   // keep their kernel-argument offsets.
   uint32_t albedo_uniform;
+  // Sparse media, the empty-region mask (round 5, cvr_set_medium_sparse): one bit
+  // per super-brick of 2^eshift cells per axis (eshift >= 3, whole leaves; bit
+  // (sz * enxy + sy * enx + sx)), set iff some leaf in it has a cell leaf, in
+  // kEmaskWords words.  Every brick word of a clear super-brick is 0 (bound code
+  // 0, the zero cell leaf: k_build_sparse_bounds), so the wave pool, which stages
+  // the mask in LDS, knows such a point's word without loading it
+  // (woodcock_point_em).  Null: no mask (every bit set; also when the bricks are
+  // unbounded, whose words are not 0).
+  const uint32_t* emask;
+  uint32_t eshift, enx, enxy;
 };
+constexpr int kEmaskWords = 64;       // sparse instances (256 B of LDS)
+constexpr int kEmaskWordsDense = 16;  // dense instances, CVR_WPOOL_EMASK_DENSE (64 B)
 
 // Brick-bound code -> bound (MediumParams::bounds): the float with bits
 // (c << 19) + (112 << 23), one v_lshl_add_u32.  c = 16 e + m stands for
@@ -539,6 +551,35 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
   }
   return P;
 }
+// woodcock_point with the empty-region mask staged in LDS (em: the first
+// kWords words of MediumParams::emask).  The same point, bound and cell
+// pointer; the brick word (sparse) or bound byte (dense) is loaded only when
+// the point's super-brick holds density: in a clear one it is 0 (sparse: bound
+// code 0, the zero cell leaf; dense: code 0), and off the grid the sentinel's
+// (255 << 24 | slot 0, or 255), all known without a load.
+template <int kWords, class EmWords>
+CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float t, const EmWords& em) {
+  WoodcockPoint P;
+  woodcock_coords(m, o, d, t, P);
+  const uint32_t x1 = (uint32_t)P.cx, y1 = (uint32_t)P.cy, z1 = (uint32_t)P.cz;
+  // (off the grid x1.. are meaningless: the word index is masked into the array)
+  const uint32_t sb = __umul24(z1 >> m.eshift, m.enxy) + __umul24(y1 >> m.eshift, m.enx) + (x1 >> m.eshift);
+  const bool load = P.in && ((em[(sb >> 5) & (uint32_t)(kWords - 1)] >> (sb & 31u)) & 1u) != 0u;
+  const uint32_t bi = __umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift);
+  if (m.sbounds) {
+    uint32_t sw = P.in ? 0u : 255u << 24;
+    if (load) sw = m.sbounds[bi];
+    P.qb = bound_value(sw >> 24);
+    P.cp = m.cells + ((((size_t)(sw & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
+  } else {
+    uint32_t q = P.in ? 0u : 255u;
+    if (load) q = m.bounds[bi];
+    P.qb = bound_value(q);
+    P.cp = m.cells + 2 * (__umul24(z1, m.rxy) + __umul24(y1, m.rx) + x1);
+  }
+  return P;
+}
+
 // The exact density at the point (cell trilinear or the 8-tap gather).
 CVR_DEV float woodcock_density(const MediumParams& m, const WoodcockPoint& P) {
   if (P.in && m.cells) {

@@ -32,6 +32,16 @@
 #ifndef CVR_WPOOL_UNROLL
 #define CVR_WPOOL_UNROLL 4
 #endif
+// Sparse media: stage the empty-region mask in LDS and skip the brick-word
+// loads of points in clear super-bricks (woodcock_point_em).
+#ifndef CVR_WPOOL_EMASK
+#define CVR_WPOOL_EMASK 1
+#endif
+// Dense media with cells and bounds likewise, with a 16-word mask (experiment,
+// DESIGN.md §6).
+#ifndef CVR_WPOOL_EMASK_DENSE
+#define CVR_WPOOL_EMASK_DENSE 0
+#endif
 // Tentative points per lane per Woodcock group (the lookahead below).  The
 // track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
 constexpr int kLook = 2;
@@ -70,12 +80,12 @@ __device__ __forceinline__ float opaque_s(float x) {
 // although the occupancy API answers 20 for all of them; 10240 B fit 16).  A
 // budget of 163840 / 20 = 8192 B therefore ran 4.5 waves per SIMD, not 5.
 constexpr int kLdsGranule = 1280;
-template <int kWaves>
+template <int kWaves, int kExtra = 0>
 struct PoolSize {
-  // LDS bytes per one-wave workgroup
+  // LDS bytes per one-wave workgroup (kExtra: bytes of it not for slots)
   static constexpr int kBudget = 163840 / (4 * kWaves) / kLdsGranule * kLdsGranule;
   static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
-  static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT) / 64;
+  static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT - kExtra) / 64;
   static_assert(4 * STAT_COUNT + 8 + 12 + 4 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
 };
 // Sparse media (C5) split the slot too and run 5 waves per SIMD: 142.7 ms vs
@@ -92,8 +102,16 @@ struct PoolSize {
 // and written once per event; so a slot takes 64 LDS bytes instead of 84 and
 // the pool holds 30% more paths, enough for 5 waves per SIMD (C2: 5.25 ms
 // vs 5.40 at 4 waves with the whole slot in LDS).
-template <int kSlots>
-struct WavePool {
+// Sparse instances also stage the medium's empty-region mask (MediumParams::
+// emask, kEm words; CVR_WPOOL_EMASK): 4 slots' worth of LDS.
+template <int kEm>
+struct EmPart {
+  uint32_t em[kEm];
+};
+template <>
+struct EmPart<0> {};
+template <int kSlots, int kEm = 0>
+struct WavePool : EmPart<kEm> {
   float4 a[kSlots], b[kSlots];
   uint4 c[kSlots];
   uint2 e[kSlots];
@@ -299,11 +317,17 @@ __device__ __forceinline__ void record_end(const LaunchParams& L, uint32_t s, co
 constexpr unsigned kWaitVm0 = 0x0F70;   // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
 constexpr uint32_t kPendAgg = 0x80000000u;  // S.pend holds kPendAgg | block << 7 | count
 
-template <int kSlots>
-__device__ __forceinline__ uint32_t count_ended(const WavePool<kSlots>& S, const LaunchParams& L, uint32_t pend,
+template <class Pool>
+__device__ __forceinline__ uint32_t count_ended(const Pool& S, const LaunchParams& L, uint32_t pend,
                                                 uint32_t lane) {
+#if defined(CVR_DIAG_NO_COUNT)  // diagnostic timing builds only: no block counts (flushers must give up)
+  (void)S; (void)L; (void)pend; (void)lane;
+  return 0u;
+#endif
   const uint32_t base = pend & 0xFFu, n = pend >> 8;
+#if !defined(CVR_DIAG_NO_COUNT_WAIT)  // diagnostic timing builds only (unordered counts)
   __builtin_amdgcn_s_waitcnt(kWaitVm0);
+#endif
   uint32_t blk = 0;
   if (lane < n) blk = tile_block_of(fresh(L), S.meta[S.ln[base + lane]]);
   const uint32_t b0 = __builtin_amdgcn_readfirstlane(blk);
@@ -322,6 +346,10 @@ __device__ __forceinline__ uint32_t count_ended(const WavePool<kSlots>& S, const
   return kPendAgg | b0 << 7 | (uint32_t)__popcll(same);
 }
 __device__ __forceinline__ void add_counted(const LaunchParams& L, uint32_t agg) {
+#if defined(CVR_DIAG_NO_COUNT)
+  (void)L; (void)agg;
+  return;
+#endif
   __hip_atomic_fetch_add(gmem(fresh(L).frame_done + kDoneStride * ((agg & ~kPendAgg) >> 7)), agg & 0x7Fu,
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -457,7 +485,10 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   // Sparse media defer their cell fetches to the end of the track iteration
   // (the lookahead below): C5 -3.0%; the dense instances lose 5-8% with it.
   constexpr bool kLookDefer = kSparse;
-  constexpr int kSlots = PoolSize<kWaves>::value;
+  constexpr int kEm = kSparse && CVR_WPOOL_EMASK                                                      ? kEmaskWords
+                      : CVR_WPOOL_EMASK_DENSE && (kMed == kMedDenseFull || kMed == kMedDenseFullUniform) ? kEmaskWordsDense
+                                                                                                         : 0;
+  constexpr int kSlots = PoolSize<kWaves, 4 * kEm>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
   // branches of the walk code fold away and take no scalar registers.
   if constexpr (kFlush) {
@@ -487,16 +518,20 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     __builtin_assume(m.sbounds != nullptr);
     m.albedo_uniform = 0u;
   }
-  static_assert(sizeof(WavePool<kSlots>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
+  static_assert(sizeof(WavePool<kSlots, kEm>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
   static_assert(kSlots <= 256, "the pool's rings and stacks hold slot indices as uint8_t");
-  __shared__ WavePool<kSlots> S;
+  __shared__ WavePool<kSlots, kEm> S;
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
   // scalars (v_readlane reloads in every Woodcock step).
   __shared__ LaunchParams L;
   const uint32_t lane = threadIdx.x;
   if (lane == 0) L = Lk;
+  if constexpr (kEm != 0) {
+    static_assert(kEm <= 64 && (kEm & (kEm - 1)) == 0, "at most one mask word per lane");
+    if (lane < (uint32_t)kEm) S.em[lane] = m.emask ? m.emask[lane] : ~0u;
+  }
   __syncthreads();
   // Counters.  Event counts are popcounts of ballots that lane 0 adds to the
   // pool's LDS counters once per batch (no per-lane registers, no SGPRs, live
@@ -628,7 +663,12 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             tk[k] = tt;
           }
 #pragma unroll
-          for (int k = 0; k < kLook; ++k) Pk[k] = woodcock_point(m, o, d, tk[k]);
+          for (int k = 0; k < kLook; ++k) {
+            if constexpr (kEm != 0)
+              Pk[k] = woodcock_point_em<kEm>(m, o, d, tk[k], S.em);
+            else
+              Pk[k] = woodcock_point(m, o, d, tk[k]);
+          }
           int end = kLook;  // the first point that ends the segment
 #pragma unroll
           for (int k = 0; k < kLook; ++k) {
@@ -1605,8 +1645,12 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, 0, s);
 }
 
+// Slots per wave of the instances a launch may run: the pool_T allocation (a
+// dense instance with a mask has fewer, its stride is its own) and the record
+// instances' path-id array (the generic dense instance, no mask).
 uint32_t wpool_slots(int waves, bool sparse) {
-  if (sparse) return waves == 5 ? PoolSize<5>::value : PoolSize<4>::value;
+  constexpr int kEmB = CVR_WPOOL_EMASK ? 4 * kEmaskWords : 0;
+  if (sparse) return waves == 5 ? PoolSize<5, kEmB>::value : PoolSize<4, kEmB>::value;
   return waves == 5   ? PoolSize<5>::value
          : waves == 6 ? PoolSize<6>::value
          : waves == 3 ? PoolSize<3>::value

@@ -2,7 +2,8 @@
 """cvr_render_frame in a process with one context (no other streams): ms per
 synchronous render, repeated (C2 by default), for the variants named in
 --variants: flush (one launch, in-launch output), copy (one launch, normalise +
-copy after it), bands2 / bands3 (2 / 3 bands of block rows, copies overlapped).
+copy after it), bands2 / bands3 (2 / 3 bands of block rows, copies overlapped),
+giveup (the in-launch output instance whose flushers leave at once).
 
   python tools/frame_probe.py [--scene manix] [--reps 20] [--variants flush,copy]
 """
@@ -40,7 +41,9 @@ def main():
     c.set_resolution(W, H)
     c.set_iterations(a.iters)
     host = torch.empty(W * H * 4, dtype=torch.float32, pin_memory=True)
-    table = {"flush": (1, 1), "copy": (1, 0), "bands2": (2, 0), "bands3": (3, 0)}
+    # giveup: the in-launch output instance with its flushers leaving at once (its block
+    # counting without the stores; the host normalises and copies after the launch)
+    table = {"flush": (1, 1), "copy": (1, 0), "bands2": (2, 0), "bands3": (3, 0), "giveup": (1, 2)}
     for rnd in range(a.rounds):
         for v in a.variants.split(","):
             parts, flush = table[v]

@@ -49,6 +49,10 @@ for step in "$@"; do
     prof:*) sc=${step#prof:}; run prof_$sc 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 10 --warmup 2 --no-cpu-baseline --no-shard-emulation ;;
     pmcf:*) sc=${step#pmcf:}; mkdir -p "$OUT/pmcf_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcf_$sc/libcvr.sha256"; run pmcf_$sc 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
     pmcw:*) sc=${step#pmcw:}; mkdir -p "$OUT/pmcw_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcw_$sc/libcvr.sha256"; run pmcw_$sc 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
+    # synchronous render variants (tools/frame_probe.py): frame:SCENE:v1,v2[:LIB]
+    frame:*) IFS=: read -r _ sc vs lib <<< "$step"; tag=default; [ -n "$lib" ] && tag=$(basename $(dirname $lib)); run frame_${sc}_$tag 400 python3 tools/frame_probe.py --scene $sc --variants $vs ${lib:+--lib $lib} ;;
+    # experiment builds (build/variants/NAME), one process each, interleaved: abr:SCENE:RES:ROUNDS:v1;v2
+    abr:*) IFS=: read -r _ sc res rounds vs <<< "$step"; run abr_${sc}_$res 900 env AB_ARGS="--res $res" bash tools/ab.sh $sc $rounds ${vs//;/ } ;;
     # VALU issue (tools/valu.py): pmcv:SCENE
     pmcv:*) sc=${step#pmcv:}; mkdir -p "$OUT/pmcv_$sc"; sha256sum cudavolumerenderer_amd/libcvr.so > "$OUT/pmcv_$sc/libcvr.sha256"; run pmcv_$sc 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- python3 "$ROOT/bench.py" --scene $sc --steps 3 --warmup 1 --no-cpu-baseline --no-shard-emulation ;;
     # one kernel id's C2 bench line: benchk:KERNEL

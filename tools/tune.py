@@ -102,6 +102,8 @@ def main():
             c.set_option(cvr.OPT_WAVE_PAIR, d["pair"])
         if "sorder" in d:
             c.set_option(cvr.OPT_SAMPLE_ORDER, d["sorder"])
+        if "em" in d:
+            c.set_option(cvr.OPT_EMPTY_MASK, d["em"])
         c.set_option(cvr.OPT_TIMING, d.get("timing", 1))
         c.init()
         c.set_resolution(W, H)
