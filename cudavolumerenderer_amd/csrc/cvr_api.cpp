@@ -869,49 +869,6 @@ int cvr_set_medium(cvr_ctx* c, const cvr_medium_desc* md) {
       m.albedo_bg = cvr::V3{md->albedo[0], md->albedo[1], md->albedo[2]};
     }
   }
-  // Empty-region mask for the dense instances that stage one
-  // (CVR_WPOOL_EMASK_DENSE, MediumParams::emask): super-bricks of 2^es cells
-  // (es >= bshift) fitting 32 kEmaskWordsDense bits; bit set iff a density
-  // corner of one of its cells (voxels [s S, min(s S + S, res - 1)] per axis)
-  // is not +-0, so that every brick code in a clear one is 0.
-  if (c->d_bounds) {
-    uint32_t es = std::max(c->bound_shift, 1u), ex, ey, ez;
-    for (;; ++es) {
-      const uint32_t S = 1u << es;
-      ex = (md->res[0] + S - 1) / S;
-      ey = (md->res[1] + S - 1) / S;
-      ez = (md->res[2] + S - 1) / S;
-      if ((uint64_t)ex * ey * ez <= 32u * cvr::kEmaskWordsDense) break;
-    }
-    std::vector<uint32_t> em(cvr::kEmaskWords, 0u);
-    const uint32_t S = 1u << es, rx = md->res[0], ry = md->res[1];
-    auto lo_hi = [&](uint32_t v, uint32_t& a, uint32_t& b) {  // super-bricks whose range holds voxel v
-      b = v >> es;
-      a = (v > 0 && (v & (S - 1)) == 0) ? b - 1 : b;
-    };
-    for (uint32_t z = 0; z < md->res[2]; ++z)
-      for (uint32_t y = 0; y < ry; ++y)
-        for (uint32_t x = 0; x < rx; ++x) {
-          const float v = md->density[((size_t)z * ry + y) * rx + x];
-          if (v == 0.0f) continue;
-          uint32_t x0, x1, y0, y1, z0, z1;
-          lo_hi(x, x0, x1);
-          lo_hi(y, y0, y1);
-          lo_hi(z, z0, z1);
-          for (uint32_t sz = z0; sz <= z1; ++sz)
-            for (uint32_t sy = y0; sy <= y1; ++sy)
-              for (uint32_t sx = x0; sx <= x1; ++sx) {
-                const uint32_t b = (sz * ey + sy) * ex + sx;
-                em[b >> 5] |= 1u << (b & 31u);
-              }
-        }
-    HIP_TRY(c, hipMalloc(&c->d_emask, em.size() * sizeof(uint32_t)));
-    HIP_TRY(c, hipMemcpy(c->d_emask, em.data(), em.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    m.eshift = es;
-    m.enx = ex;
-    m.enxy = ex * ey;
-    m.emask = c->d_emask;
-  }
   c->have_medium = true;
   return CVR_OK;
 }

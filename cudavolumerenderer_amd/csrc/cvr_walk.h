@@ -184,8 +184,7 @@ struct MediumParams {
   const uint32_t* emask;
   uint32_t eshift, enx, enxy;
 };
-constexpr int kEmaskWords = 64;       // sparse instances (256 B of LDS)
-constexpr int kEmaskWordsDense = 16;  // dense instances, CVR_WPOOL_EMASK_DENSE (64 B)
+constexpr int kEmaskWords = 64;
 
 // Brick-bound code -> bound (MediumParams::bounds): the float with bits
 // (c << 19) + (112 << 23), one v_lshl_add_u32.  c = 16 e + m stands for
@@ -551,12 +550,11 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
   }
   return P;
 }
-// woodcock_point with the empty-region mask staged in LDS (em: the first
-// kWords words of MediumParams::emask).  The same point, bound and cell
-// pointer; the brick word (sparse) or bound byte (dense) is loaded only when
-// the point's super-brick holds density: in a clear one it is 0 (sparse: bound
-// code 0, the zero cell leaf; dense: code 0), and off the grid the sentinel's
-// (255 << 24 | slot 0, or 255), all known without a load.
+// woodcock_point on a sparse medium with the empty-region mask staged in LDS
+// (em: MediumParams::emask's kWords words).  The same point, bound and cell
+// pointer; the brick word is loaded only when the point's super-brick has a
+// cell leaf: in a clear one it is 0 (bound code 0, the zero cell leaf), and off
+// the grid the sentinel's (255 << 24, slot 0), both known without a load.
 template <int kWords, class EmWords>
 CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float t, const EmWords& em) {
   WoodcockPoint P;
@@ -565,18 +563,10 @@ CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float
   // (off the grid x1.. are meaningless: the word index is masked into the array)
   const uint32_t sb = __umul24(z1 >> m.eshift, m.enxy) + __umul24(y1 >> m.eshift, m.enx) + (x1 >> m.eshift);
   const bool load = P.in && ((em[(sb >> 5) & (uint32_t)(kWords - 1)] >> (sb & 31u)) & 1u) != 0u;
-  const uint32_t bi = __umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift);
-  if (m.sbounds) {
-    uint32_t sw = P.in ? 0u : 255u << 24;
-    if (load) sw = m.sbounds[bi];
-    P.qb = bound_value(sw >> 24);
-    P.cp = m.cells + ((((size_t)(sw & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
-  } else {
-    uint32_t q = P.in ? 0u : 255u;
-    if (load) q = m.bounds[bi];
-    P.qb = bound_value(q);
-    P.cp = m.cells + 2 * (__umul24(z1, m.rxy) + __umul24(y1, m.rx) + x1);
-  }
+  uint32_t sw = P.in ? 0u : 255u << 24;
+  if (load) sw = m.sbounds[__umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift)];
+  P.qb = bound_value(sw >> 24);
+  P.cp = m.cells + ((((size_t)(sw & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
   return P;
 }
 

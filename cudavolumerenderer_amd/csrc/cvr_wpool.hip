@@ -37,11 +37,6 @@
 #ifndef CVR_WPOOL_EMASK
 #define CVR_WPOOL_EMASK 1
 #endif
-// Dense media with cells and bounds likewise, with a 16-word mask (experiment,
-// DESIGN.md §6).
-#ifndef CVR_WPOOL_EMASK_DENSE
-#define CVR_WPOOL_EMASK_DENSE 0
-#endif
 // Tentative points per lane per Woodcock group (the lookahead below).  The
 // track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
 constexpr int kLook = 2;
@@ -485,9 +480,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   // Sparse media defer their cell fetches to the end of the track iteration
   // (the lookahead below): C5 -3.0%; the dense instances lose 5-8% with it.
   constexpr bool kLookDefer = kSparse;
-  constexpr int kEm = kSparse && CVR_WPOOL_EMASK                                                      ? kEmaskWords
-                      : CVR_WPOOL_EMASK_DENSE && (kMed == kMedDenseFull || kMed == kMedDenseFullUniform) ? kEmaskWordsDense
-                                                                                                         : 0;
+  // (dense media: +7% C2, +6% C3 with a 16-word mask)
+  constexpr int kEm = kSparse && CVR_WPOOL_EMASK ? kEmaskWords : 0;
   constexpr int kSlots = PoolSize<kWaves, 4 * kEm>::value;
   // Dense instances see the sparse pointers as constant null, so the sparse
   // branches of the walk code fold away and take no scalar registers.
@@ -529,8 +523,8 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   const uint32_t lane = threadIdx.x;
   if (lane == 0) L = Lk;
   if constexpr (kEm != 0) {
-    static_assert(kEm <= 64 && (kEm & (kEm - 1)) == 0, "at most one mask word per lane");
-    if (lane < (uint32_t)kEm) S.em[lane] = m.emask ? m.emask[lane] : ~0u;
+    static_assert(kEm == 64, "one mask word per lane");
+    S.em[lane] = m.emask ? m.emask[lane] : ~0u;
   }
   __syncthreads();
   // Counters.  Event counts are popcounts of ballots that lane 0 adds to the
@@ -1645,9 +1639,6 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, 0, s);
 }
 
-// Slots per wave of the instances a launch may run: the pool_T allocation (a
-// dense instance with a mask has fewer, its stride is its own) and the record
-// instances' path-id array (the generic dense instance, no mask).
 uint32_t wpool_slots(int waves, bool sparse) {
   constexpr int kEmB = CVR_WPOOL_EMASK ? 4 * kEmaskWords : 0;
   if (sparse) return waves == 5 ? PoolSize<5, kEmB>::value : PoolSize<4, kEmB>::value;
