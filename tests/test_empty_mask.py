@@ -82,3 +82,29 @@ def test_empty_mask_records_bit_exact(cvr, oracle_mod):
     c = orc.trace_paths(orc.launch(iv, r2v, (W, H), (W, H), (0, 0), 2, 0), 0, n)
     _compare(g, c, "emask es 5 records", mixed=False)
     ctx.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bounds,cells", [(0, 1), (1, 1), (2, 0), (3, 0)])
+def test_empty_mask_brick_and_cell_layouts(cvr, bounds, cells):
+    """Brick sizes 2^3..8^3 (CVR_OPT_BOUNDS 1-3; 0: unbounded, so no mask: the
+    words of empty bricks are then 255 << 24) and the 8-tap gather instead of
+    cells: the mask only skips loads whose word it knows."""
+    scene = cvr.Scene.synthetic("cloud", 0, (96, 48, 104))
+    W, H, iters = 128, 96, 3
+    out = []
+    for em in (1, 0):
+        c = cvr.Context(0, "regenerationSK")
+        c.set_option(cvr.OPT_BOUNDS, bounds)
+        c.set_option(cvr.OPT_CELLS, cells)
+        c.set_medium_sparse(scene.sparse_medium)
+        iv, r2v = cvr.default_camera(W, H)
+        c.set_camera(iv, r2v, (W, H))
+        c.init()
+        c.set_option(cvr.OPT_EMPTY_MASK, em)
+        out.append(c.render_image(W, H, (1, 1), iters))
+        c.close()
+    (i1, s1), (i0, s0) = out
+    for k in COUNTERS + ("fetches",):
+        assert getattr(s1, k) == getattr(s0, k), k
+    assert_pixels_close(i1, i0, iters, f"bounds {bounds} cells {cells}: mask vs every word loaded")
