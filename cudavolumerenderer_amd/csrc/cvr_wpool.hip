@@ -37,13 +37,12 @@
 #ifndef CVR_WPOOL_EMASK
 #define CVR_WPOOL_EMASK 1
 #endif
-// Dense instances: one cell-fetch block per Woodcock group (experiment)
-#ifndef CVR_WPOOL_ONE_FETCH
-#define CVR_WPOOL_ONE_FETCH 0
-#endif
 // Tentative points per lane per Woodcock group (the lookahead below).  The
 // track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
-constexpr int kLook = 2;
+#ifndef CVR_WPOOL_LOOK
+#define CVR_WPOOL_LOOK 2
+#endif
+constexpr int kLook = CVR_WPOOL_LOOK;
 // The track loop runs CVR_WPOOL_UNROLL / kLook groups: a variant build with
 // UNROLL < kLook would run none (tracking lanes never step: the launch never
 // ends), one with a remainder would silently drop the remainder's steps.
@@ -668,57 +667,6 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
               Pk[k] = woodcock_point(m, o, d, tk[k]);
           }
           int end = kLook;  // the first point that ends the segment
-#if CVR_WPOOL_ONE_FETCH
-          if constexpr (!kLookDefer) {
-            // one fetch block per group for each lane's first point that needs its
-            // cell (the later points after a null collision in a second, rare one)
-            int kf = kLook;
-#pragma unroll
-            for (int k = 0; k < kLook; ++k) {
-              if (end == kLook && kf == kLook) {
-                if (!(tk[k] <= max_t)) {
-                  fst = 1;
-                  end = k;
-                } else if (!(Pk[k].qb < xtk[k])) {
-                  kf = k;
-                }
-              }
-            }
-            if (kf < kLook) {
-              WoodcockPoint Pf = Pk[0];
-              float xf = xtk[0];
-#pragma unroll
-              for (int k = 1; k < kLook; ++k)
-                if (kf == k) {
-                  Pf = Pk[k];
-                  xf = xtk[k];
-                }
-              ++c_fetch;
-              const float rho = m.scale * woodcock_density(m, Pf);
-              if (!(rho * m.inv_sigma < xf)) {
-                fst = 2;
-                end = kf;
-              } else {
-#pragma unroll
-                for (int k = 1; k < kLook; ++k) {
-                  if (end == kLook && k > kf) {
-                    if (!(tk[k] <= max_t)) {
-                      fst = 1;
-                      end = k;
-                    } else if (!(Pk[k].qb < xtk[k])) {
-                      ++c_fetch;
-                      const float rho2 = m.scale * woodcock_density(m, Pk[k]);
-                      if (!(rho2 * m.inv_sigma < xtk[k])) {
-                        fst = 2;
-                        end = k;
-                      }
-                    }
-                  }
-                }
-              }
-            }
-          } else
-#endif
 #pragma unroll
           for (int k = 0; k < kLook; ++k) {
             if (end == kLook) {
