@@ -143,7 +143,7 @@ struct cvr_ctx {
   int wpool_waves = 0;
   int morton = 0;  // CVR_OPT_MORTON
   int wave_pair = 0;  // CVR_OPT_WAVE_PAIR
-  int sample_order = -1;  // CVR_OPT_SAMPLE_ORDER (-1: 1 for a sparse medium, else 0)
+  int sample_order = -1;  // CVR_OPT_SAMPLE_ORDER (-1: the default, 0)
   int empty_mask = 1;     // CVR_OPT_EMPTY_MASK
   uint32_t swap_batch = 8;
   int track_grid = 0;
@@ -1369,13 +1369,15 @@ int cvr_launch_render(cvr_ctx* c) {
   }
   if (scheduler_for(c) == 3) {
     L.wflags = (uint32_t)(c->drain < 0 ? 1 : c->drain) & cvr::kDrainMask;
-    // samples innermost + combined splats: C5 -1.4% (123.0 vs 124.7 ms), dense C2 / C3 +2.7% /
-    // +3.6% (profiles/round5/ab/call6_sample_order_ab.log, call7): on by default for sparse media
-    // The in-launch output instance (cvr_render_frame) splats per lane (combining cost its
-    // dense instance two VGPR spills), and per-lane splats with samples innermost put the same
-    // pixel on several lanes of one atomic instruction, which the memory side serialises (C5 one
-    // render 2086 vs 2666 Msamples/s): that launch keeps the sample-major order.
-    int so = c->sample_order >= 0 ? c->sample_order : (c->m.leaves != nullptr ? 1 : 0);
+    // samples innermost + combined splats (CVR_OPT_SAMPLE_ORDER 1): dense C2 / C3 +2.7% / +3.6%
+    // (profiles/round5/ab/call6_sample_order_ab.log); C5 -1.4% before the sparse empty-region
+    // mask, +2.2% with it (116.4-116.8 vs 118.9-119.7 ms, profiles/round5/ab/
+    // c5_sample_order_emask.log): off by default.  The in-launch output instance
+    // (cvr_render_frame) splats per lane (combining cost its dense instance two VGPR spills), and
+    // per-lane splats with samples innermost put the same pixel on several lanes of one atomic
+    // instruction, which the memory side serialises (C5 one render 2086 vs 2666 Msamples/s):
+    // that launch always keeps the sample-major order.
+    int so = c->sample_order >= 0 ? c->sample_order : 0;
     if (c->frame_done_active) so = 0;
     if (so == 1) L.wflags |= cvr::kUnitSampleInner | cvr::kSplatCombine;
   }

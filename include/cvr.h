@@ -66,14 +66,15 @@ typedef enum {
   CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
   CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
   CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
-  CVR_OPT_SCHEDULER = 6,      /* how paths map onto threads, for every kernel id but naiveMK:
-                                 0 single persistent kernel, 1 wavefront pair (streamingMK's
-                                 multi-kernel structure), 2 workgroup path pool in LDS (streamingSK's
-                                 block streaming), 3 wave-private path pool in LDS (the default for
-                                 all of them; round 4 and before: naiveSK 4, streamingSK 2,
-                                 streamingMK 1), 4 one path per work-item (naiveSK's structure).
-                                 Scheduling only: results depend on the kernel id, not on the
-                                 scheduler. */
+  CVR_OPT_SCHEDULER = 6,      /* how paths map onto threads: 0 single persistent kernel, 1 wavefront
+                                 pair (streamingMK's multi-kernel structure), 2 workgroup path pool
+                                 in LDS (streamingSK's block streaming), 3 wave-private path pool in
+                                 LDS (the default for every kernel id; round 4 and before: naiveSK 4,
+                                 streamingSK 2, streamingMK 1, naiveMK its own per-item kernel), 4 one
+                                 path per work-item (naiveSK's structure; naiveMK: k_naive_mk).
+                                 naiveMK runs the wave pool with 3 and k_naive_mk with any other
+                                 value (its per-bounce kernels with CVR_OPT_MK_COMPACTION 1).  Scheduling only: results depend on the
+                                 kernel id, not on the scheduler. */
   CVR_OPT_POOL = 7,           /* wavefront ray-slot pool size (default 2^21) */
   CVR_OPT_TIMING = 8,         /* 1: time every wavefront kernel (track_ms / events_ms) */
   CVR_OPT_CELLS = 9           /* 1 (default): corner-replicated density cells (8x density bytes
@@ -147,8 +148,8 @@ typedef enum {
                                  with the samples innermost, and each event batch sums its escapes per
                                  pixel before the framebuffer atomics (C3: 2.23 -> 0.99 GB written per
                                  launch; a launch with cvr_render_frame's in-launch output keeps
-                                 order 0 and per-lane atomics).  -1 (default): 1 for a sparse medium (C5 -1.4%), 0 for a
-                                 dense one (C2 / C3 +2.7% / +3.6% with 1).
+                                 order 0 and per-lane atomics).  -1 (default) = 0: order 1 costs C2 / C3 2.7% / 3.6%
+                                 and C5 2.2% (with the empty-region mask).
                                  Scheduling and summation order only. */
   CVR_OPT_WAVE_PAIR = 26,      /* wave-pool scheduler, dense media with cells and bounds: 1 runs two waves
                                  per workgroup whose boundary and collision event lists are shared

@@ -3,8 +3,9 @@ samples innermost, and the event batch's per-pixel combining of escapes
 before the framebuffer atomics (splat_wave).  Scheduling and summation order
 only: against the sample-major order (0) and the oracle the counters must be
 equal, every production path's record bit-exact, and the pixels within the
-summation-order bound.  Sparse media run order 1 by default,
-dense ones order 0."""
+summation-order bound.  Order 0 is the default (order 1 ran
+sparse media by default until the empty-region mask made order 0 faster there
+too)."""
 import numpy as np
 import pytest
 
