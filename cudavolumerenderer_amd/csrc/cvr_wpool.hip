@@ -39,6 +39,11 @@
 #endif
 // Tentative points per lane per Woodcock group (the lookahead below).  The
 // track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
+// Sparse instances: a point that needs its cell parks until the end of the track
+// iteration (kLookDefer below).
+#ifndef CVR_WPOOL_SPARSE_DEFER
+#define CVR_WPOOL_SPARSE_DEFER 1
+#endif
 #ifndef CVR_WPOOL_LOOK
 #define CVR_WPOOL_LOOK 2
 #endif
@@ -482,7 +487,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   constexpr bool kSparse = kMed == kMedSparse;
   // Sparse media defer their cell fetches to the end of the track iteration
   // (the lookahead below): C5 -3.0%; the dense instances lose 5-8% with it.
-  constexpr bool kLookDefer = kSparse;
+  constexpr bool kLookDefer = kSparse && CVR_WPOOL_SPARSE_DEFER;
   // (dense media: +7% C2, +6% C3 with a 16-word mask)
   constexpr int kEm = kSparse && CVR_WPOOL_EMASK ? kEmaskWords : 0;
   constexpr int kSlots = PoolSize<kWaves, 4 * kEm>::value;
