@@ -970,15 +970,21 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
     e = cvr::launch_build_sparse(m, d_coords, c->use_cells ? ncl : 0, d_slot, bnz, sd->max_density, unbounded,
                                  c->d_cells, c->d_sbounds, c->stream);
   // Empty-region mask (MediumParams::emask): the smallest super-brick of 2^es
-  // cells per axis whose grid fits 32 kEmaskWords bits; bit set iff a leaf in it
-  // has a cell leaf.  Clear super-bricks' brick words are 0 only when bounded.
+  // cells per axis whose grid, each axis padded to a power of two, fits 32
+  // kEmaskWords bits; bit set iff a leaf in it has a cell leaf.  Clear
+  // super-bricks' brick words are 0 only when bounded.
   if (e == hipSuccess && !unbounded) {
-    uint32_t es = 3, ex = lnx, ey = lny, ez = lnz;
-    while ((uint64_t)ex * ey * ez > 32u * cvr::kEmaskWords) {
+    auto log2up = [](uint32_t v) {
+      uint32_t l = 0;
+      while ((1u << l) < v) ++l;
+      return l;
+    };
+    uint32_t es = 3, lx = log2up(lnx), ly = log2up(lny), lz = log2up(lnz);
+    while (lx + ly + lz > log2up(32u * cvr::kEmaskWords)) {
       ++es;
-      ex = (ex + 1) / 2;
-      ey = (ey + 1) / 2;
-      ez = (ez + 1) / 2;
+      lx -= lx > 0;
+      ly -= ly > 0;
+      lz -= lz > 0;
     }
     std::vector<uint32_t> em(cvr::kEmaskWords, 0u);
     const uint32_t k = es - 3;
@@ -986,14 +992,14 @@ int cvr_set_medium_sparse(cvr_ctx* c, const cvr_sparse_medium_desc* sd) {
       for (uint32_t y = 0; y < lny; ++y)
         for (uint32_t x = 0; x < lnx; ++x)
           if (cell_slot[((size_t)z * lny + y) * lnx + x] != 0u) {
-            const uint32_t b = ((z >> k) * ey + (y >> k)) * ex + (x >> k);
+            const uint32_t b = (z >> k) << (lx + ly) | (y >> k) << lx | (x >> k);
             em[b >> 5] |= 1u << (b & 31u);
           }
     e = hipMalloc(&c->d_emask, em.size() * sizeof(uint32_t));
     if (e == hipSuccess) e = hipMemcpy(c->d_emask, em.data(), em.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     m.eshift = es;
-    m.enx = ex;
-    m.enxy = ex * ey;
+    m.eshy = lx;
+    m.eshz = lx + ly;
     m.emask = c->d_emask;
   }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

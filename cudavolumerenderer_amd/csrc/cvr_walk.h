@@ -174,15 +174,15 @@ struct MediumParams {
   // keep their kernel-argument offsets.
   uint32_t albedo_uniform;
   // Sparse media, the empty-region mask (round 5, cvr_set_medium_sparse): one bit
-  // per super-brick of 2^eshift cells per axis (eshift >= 3, whole leaves; bit
-  // (sz * enxy + sy * enx + sx)), set iff some leaf in it has a cell leaf, in
-  // kEmaskWords words.  Every brick word of a clear super-brick is 0 (bound code
+  // per super-brick of 2^eshift cells per axis (eshift >= 3, whole leaves), the
+  // super-brick grid padded to powers of two per axis, bit sz << eshz | sy << eshy
+  // | sx, set iff some leaf in it has a cell leaf, in kEmaskWords words.  Every brick word of a clear super-brick is 0 (bound code
   // 0, the zero cell leaf: k_build_sparse_bounds), so the wave pool, which stages
   // the mask in LDS, knows such a point's word without loading it
   // (woodcock_point_em).  Null: no mask (every bit set; also when the bricks are
   // unbounded, whose words are not 0).
   const uint32_t* emask;
-  uint32_t eshift, enx, enxy;
+  uint32_t eshift, eshy, eshz;
 };
 constexpr int kEmaskWords = 64;
 
@@ -560,9 +560,11 @@ CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float
   WoodcockPoint P;
   woodcock_coords(m, o, d, t, P);
   const uint32_t x1 = (uint32_t)P.cx, y1 = (uint32_t)P.cy, z1 = (uint32_t)P.cz;
-  // (off the grid x1.. are meaningless: the word index is masked into the array)
-  const uint32_t sb = __umul24(z1 >> m.eshift, m.enxy) + __umul24(y1 >> m.eshift, m.enx) + (x1 >> m.eshift);
-  const bool load = P.in && ((em[(sb >> 5) & (uint32_t)(kWords - 1)] >> (sb & 31u)) & 1u) != 0u;
+  // (off the grid x1.. are meaningless: the word index is masked into the array,
+  // so the LDS read needs no branch; shifts and v_lshl_or, no multiplies)
+  const uint32_t sb = ((z1 >> m.eshift) << m.eshz) | ((y1 >> m.eshift) << m.eshy) | (x1 >> m.eshift);
+  const uint32_t word = em[(sb >> 5) & (uint32_t)(kWords - 1)];
+  const bool load = P.in & (__builtin_amdgcn_ubfe(word, sb & 31u, 1u) != 0u);
   uint32_t sw = P.in ? 0u : 255u << 24;
   if (load) sw = m.sbounds[__umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift)];
   P.qb = bound_value(sw >> 24);

@@ -25,8 +25,10 @@ def mask_bits(scene):
         for dy in (0, 1):
             for dx in (0, 1):
                 cell[:lz - dz, :ly - dy, :lx - dx] |= occ[dz:, dy:, dx:]
+    # each axis of the super-brick grid padded to a power of two (the kernel's
+    # index is sz << eshz | sy << eshy | sx)
     k = 0
-    while (-(-lz >> k)) * (-(-ly >> k)) * (-(-lx >> k)) > EMASK_BITS:
+    while sum((-(-n >> k) - 1).bit_length() for n in (lz, ly, lx)) > EMASK_BITS.bit_length() - 1:
         k += 1
     ez, ey, ex = (-(-n // (1 << k)) for n in (lz, ly, lx))
     pad = np.zeros((ez << k, ey << k, ex << k), bool)
