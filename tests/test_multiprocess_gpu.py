@@ -30,19 +30,25 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("shard,tiles", [("paths", (1, 1)), ("tilepaths", (2, 2))])
-def test_two_ranks_one_gpu_bench_step_equals_single_render(cvr, tmp_path, shard, tiles):
+# "bare": the driver's own command, `python3 bench.py --gpus 2 ...` with no launcher: bench.py
+# starts its two ranks itself (spawn_ranks); "torchrun": the torch.distributed.run form
+@pytest.mark.parametrize("shard,tiles,launcher", [("paths", (1, 1), "bare"), ("tilepaths", (2, 2), "torchrun")])
+def test_two_ranks_one_gpu_bench_step_equals_single_render(cvr, tmp_path, shard, tiles, launcher):
     W = H = 256
     iters = 4
     out = str(tmp_path / "img.npy")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "gloo", "--same-device",
+    pre = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] if launcher == "torchrun" else \
+          [sys.executable]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = pre + [os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--backend", "gloo", "--same-device",
            "--resolution", str(W), str(H), "--iterations", str(iters), "--shard", shard,
            "--number-of-tiles", str(tiles[0]), str(tiles[1]), "--no-cpu-baseline", "--dump-image", out]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    js = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(js) == 1, r.stdout[-3000:]  # one JSON line: rank 0's, relayed
+    line = json.loads(js[0])
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["value"] > 0
     if shard == "paths":
         assert line["weak"]["value"] > 0
