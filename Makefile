@@ -63,3 +63,8 @@ variant: $(SRCS_HIP) $(SRCS_CPP) $(HDRS)
 	@mkdir -p build/variants/$(NAME)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -shared -o build/variants/$(NAME)/libcvr.so $(SRCS_HIP) $(patsubst %,-x hip %,$(SRCS_CPP)) -lz
 .PHONY: variant
+# The workgroup-shared event-list experiment (k_wpair), kept out of libcvr.so:
+#   make variant-pair; CVR_LIB=build/variants/pair/libcvr.so pytest tests/test_wave_pair.py -m gpu
+variant-pair:
+	$(MAKE) variant NAME=pair DEFS="-DCVR_WPOOL_PAIR=1"
+.PHONY: variant-pair

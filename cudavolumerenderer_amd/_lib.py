@@ -14,8 +14,10 @@ from typing import Optional, Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcvr.so")
-_DEFAULT_LIB = os.path.abspath(LIB_PATH)
+_DEFAULT_LIB = os.path.abspath(os.path.join(_HERE, "libcvr.so"))
+# CVR_LIB: an experiment build instead of the in-tree library (e.g. `make variant-pair`'s,
+# for tests/test_wave_pair.py); unset, the in-tree libcvr.so
+LIB_PATH = os.environ.get("CVR_LIB") or _DEFAULT_LIB
 
 CVR_OK = 0
 ERRORS = {-1: "CVR_ERR_INVALID", -2: "CVR_ERR_HIP", -3: "CVR_ERR_STATE", -4: "CVR_ERR_IO",
@@ -509,16 +511,16 @@ class Context:
                      host: bool = True):
         return self.render_tiles(width, height, n_tiles, iterations, 0, 1, device_image, host)
 
-    def render_frame(self, host_ptr: Optional[int] = None, parts: int = 0, stats: bool = True,
+    def render_frame(self, host_ptr=None, parts: int = 0, stats: bool = True,
                      host_floats: Optional[int] = None):
         """CudaVolPath::render for one tile (cvr_render_frame): clear, render
         the set resolution / iterations, and the normalised image in host
         memory when it returns, the launch split into `parts` bands whose
-        copies overlap the later bands.  host_ptr: a width*height*4 float
-        buffer (pinned for asynchronous copies); None returns a new array.
-        stats=False skips the counters (one synchronous read per band).
-        host_floats: the floats host_ptr holds (the library rejects a buffer
-        shorter than the tile; default: exactly the tile, width*height*4)."""
+        copies overlap the later bands.  host_ptr: a PinnedImage, or the
+        address of a float buffer (pinned for asynchronous copies) together
+        with host_floats, the floats it holds (the library rejects a buffer
+        shorter than the tile); None returns a new array.  stats=False skips
+        the counters (one synchronous read per band)."""
         st = Stats() if stats else None
         img = None
         w, h = self.resolution  # the library's own tile size (what cvr_render_frame writes)
@@ -528,8 +530,13 @@ class Context:
             img = np.zeros((h, w, 4), np.float32)
             host_ptr = img.ctypes.data
             host_floats = img.size
-        if host_floats is None:
-            host_floats = w * h * 4
+        elif isinstance(host_ptr, PinnedImage):
+            host_floats = host_ptr.floats if host_floats is None else host_floats
+            host_ptr = host_ptr.ptr.value
+        elif host_floats is None:
+            # a bare address says nothing about its size: the caller states it, so the library's
+            # size check (ABI 3) always runs
+            raise CvrError(-1, "render_frame: host_floats is required with a raw host_ptr")
         self._c(load().cvr_render_frame(self._h, C.c_void_p(host_ptr), host_floats, parts,
                                         C.byref(st) if stats else None))
         return img, st
@@ -605,3 +612,17 @@ class PinnedImage:
         if self.ptr:
             load().cvr_host_free(self.ptr)
             self.ptr = C.c_void_p()
+            self.array = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 (interpreter shutdown: the library may be gone)
+            pass

@@ -1266,6 +1266,9 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       return CVR_OK;
     case CVR_OPT_WAVE_PAIR:
       if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "wave pair must be 0 or 1");
+      if (v == 1 && !cvr::wpool_pair_built())
+        return set_err(&c->err, CVR_ERR_UNSUPPORTED,
+                       "wave pair (k_wpair) is an experiment built only into `make variant-pair`");
       c->wave_pair = (int)v;
       return CVR_OK;
     case CVR_OPT_UNIFORM_ALBEDO:
@@ -1775,6 +1778,19 @@ int cvr_render_share_to_host(cvr_ctx* c, const cvr_render_desc* d, uint32_t firs
   if ((r = cvr_set_resolution(c, W, H)) || (r = cvr_set_iterations(c, d->iterations)) || (r = cvr_set_offset(c, 0, 0)))
     return r;
   if ((r = check_ready(c)) || (r = ensure_output(c))) return r;
+  {
+    // the launch must really be this context's 8x8-block shard: fill_launch falls back to a
+    // contiguous slice of path ids (part-sums of other pixels) without the block work order
+    // (thread-bound RNG, CVR_OPT_ORDER 0, the per-item / wavefront schedulers, > 2^20 samples)
+    uint64_t first = 0, count = 0;
+    compute_range(c, &first, &count);
+    cvr::LaunchParams Lc{};
+    fill_launch(c, Lc, first, count);
+    if (c->shard_world > 1 && (Lc.order != 1 || Lc.blk_stride != c->shard_world || c->rng_binding != 0))
+      return set_err(&c->err, CVR_ERR_UNSUPPORTED,
+                     "this launch has no 8x8-block work order (thread-bound RNG, CVR_OPT_ORDER 0, a per-item or "
+                     "wavefront scheduler, or more than 2^20 samples), so it cannot be block-sharded over devices");
+  }
   if ((r = cvr_clear_output(c)) || (r = cvr_launch_render(c))) return r;
   e = cvr::launch_blocks_to_host(reinterpret_cast<const float*>(c->d_out), static_cast<float*>(dhost), W, H,
                                  c->shard_rank, c->shard_world, (float)d->iterations, c->stream);

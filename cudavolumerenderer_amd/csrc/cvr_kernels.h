@@ -52,6 +52,8 @@ hipError_t launch_trace(const MediumParams& m, const LaunchParams& L, bool scatt
                         hipStream_t s);
 hipError_t launch_pool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid, hipStream_t s);
 hipError_t pool_occupancy(bool scatter_eps, int* blocks_per_cu);
+// whether this build carries k_wpair (CVR_WPOOL_PAIR; only `make variant-pair`)
+bool wpool_pair_built();
 // pair: two waves per workgroup sharing their event lists (k_wpair; dense media with
 // cells and bounds, 5 waves per SIMD, no records / in-launch output; else k_wpool).
 // naive_mk: naiveMK's walk on the wave pool (5 waves per SIMD, no records / in-launch output).

@@ -65,7 +65,8 @@ void usage() {
       "  --device N, --seed S\n"
       "  --devices N|d0,d1,...              render on several devices at once (one context and host\n"
       "                                     thread each; ids may repeat): tile k -> device k mod N\n"
-      "                                     with --number-of-tiles, else 8x8-block shards of the image\n"
+      "                                     with --number-of-tiles, else 8x8-block shards of the image;\n"
+      "                                     one value is a count (pick one device with --device)\n"
       "  --pfm                              also write the float image as <output>.pfm\n"
       "  --rng-binding path|thread (=path)  regenerationSK: thread = the reference's Rng(seed + tid)\n"
       "                                     per persistent thread (non-deterministic, SURVEY Q2)\n"
@@ -138,20 +139,31 @@ int parse(int argc, char** argv, Options& o) {
   return 0;
 }
 
-// --devices: "N" (devices first..first+N-1) or "d0,d1,..." (ids may repeat: several
-// contexts on one device, each with its own stream and work queues)
+// --devices: "N" (devices first..first+N-1; a single value is always a count: one
+// device is chosen with --device) or "d0,d1,..." (two or more ids, which may repeat:
+// several contexts on one device, each with its own stream and work queues).  An
+// empty or non-numeric entry is an error (empty result).
+bool parse_uint(const std::string& s, unsigned& v) {
+  if (s.empty() || s.size() > 9) return false;
+  for (char ch : s)
+    if (ch < '0' || ch > '9') return false;
+  v = (unsigned)strtoul(s.c_str(), nullptr, 10);
+  return true;
+}
 std::vector<int> parse_devices(const std::string& v, unsigned first) {
   std::vector<int> d;
   if (v.empty()) return {(int)first};
+  unsigned x = 0;
   if (v.find(',') == std::string::npos) {
-    const unsigned n = (unsigned)strtoul(v.c_str(), nullptr, 10);
-    for (unsigned k = 0; k < n; ++k) d.push_back((int)(first + k));
+    if (!parse_uint(v, x) || x == 0) return {};
+    for (unsigned k = 0; k < x; ++k) d.push_back((int)(first + k));
     return d;
   }
   size_t p = 0;
   while (p <= v.size()) {
     const size_t q = std::min(v.find(',', p), v.size());
-    d.push_back((int)strtoul(v.substr(p, q - p).c_str(), nullptr, 10));
+    if (!parse_uint(v.substr(p, q - p), x)) return {};
+    d.push_back((int)x);
     p = q + 1;
   }
   return d;
@@ -294,7 +306,8 @@ int main(int argc, char** argv) {
   };
   const std::vector<int> devs = parse_devices(o.devices, o.device);
   if (devs.empty()) {
-    fprintf(stderr, "[ConfigParser] Error: --devices needs a count or a list of device ids\n");
+    fprintf(stderr, "[ConfigParser] Error: --devices needs a count (N >= 1) or a list of two or more device ids "
+                    "(d0,d1,...), digits only\n");
     return 2;
   }
   const unsigned ntiles = o.tiles[0] * o.tiles[1];
@@ -303,6 +316,12 @@ int main(int argc, char** argv) {
   if (n_dev > 1 && !tile_mode && (W % 8 || H % 8)) {
     printf("[Devices] one tile of %ux%u: block shards need sides that are multiples of 8; rendering on device %d\n", W,
            H, devs[0]);
+    n_dev = 1;
+  }
+  if (n_dev > 1 && !tile_mode && o.rng_binding == "thread") {
+    // the thread-bound RNG has no 8x8-block work order (cvr_render_share_to_host refuses it)
+    printf("[Devices] --rng-binding thread renders paths in launch order, not in 8x8 blocks: no block shards; "
+           "rendering on device %d\n", devs[0]);
     n_dev = 1;
   }
   if (n_dev > 1) {
@@ -360,10 +379,18 @@ int main(int argc, char** argv) {
           fprintf(stderr, "Error (context %zu, device %d): %s\n", k, devs[k], errs[k].c_str());
           return 1;
         }
+        // every counter summed, as cvr_render_tiles sums its tiles'
         st.paths += sts[k].paths;
         st.segments += sts[k].segments;
         st.steps += sts[k].steps;
+        st.density += sts[k].density;
+        st.albedo += sts[k].albedo;
         st.escaped += sts[k].escaped;
+        st.truncated += sts[k].truncated;
+        st.fetches += sts[k].fetches;
+        st.iterations += sts[k].iterations;
+        st.track_ms += sts[k].track_ms;
+        st.events_ms += sts[k].events_ms;
         st.kernel_ms = std::max(st.kernel_ms, sts[k].kernel_ms);
       }
     }

@@ -44,6 +44,11 @@
 #ifndef CVR_WPOOL_SPARSE_DEFER
 #define CVR_WPOOL_SPARSE_DEFER 1
 #endif
+// The workgroup-shared event lists (k_wpair, CVR_OPT_WAVE_PAIR): an experiment
+// that lost 4.1x, built only into `make variant-pair`.
+#ifndef CVR_WPOOL_PAIR
+#define CVR_WPOOL_PAIR 0
+#endif
 #ifndef CVR_WPOOL_LOOK
 #define CVR_WPOOL_LOOK 2
 #endif
@@ -1065,6 +1070,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   }
 }
 
+#if CVR_WPOOL_PAIR  // experiment build only: make variant-pair (round-6 verdict: 4.1x slower, not in libcvr.so)
 // ---- workgroup-shared event lists (CVR_OPT_WAVE_PAIR 1, round 5) ------------
 // The round-3/4 verdicts' "event list shared by the waves of a workgroup": two
 // waves per workgroup, one unified slot array (2 x kPairSlots paths), each wave
@@ -1573,6 +1579,8 @@ __global__ __launch_bounds__(128, kWaves) void k_wpair(MediumParams mk, LaunchPa
   }
 }
 
+#endif  // CVR_WPOOL_PAIR
+
 // Instances: 5 waves per SIMD (the default budget) for every medium layout, with and
 // without the in-launch output; the other budgets for the generic layouts.
 template <bool E>
@@ -1626,6 +1634,7 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
     void* args[] = {&mm, &ll};
     return hipLaunchKernel(wpool_mk_fn(sparse, full, uniform), dim3(grid), dim3(64), args, 0, s);
   }
+#if CVR_WPOOL_PAIR
   if (pair && waves == 5 && full && !flush && !L.rec && grid >= 2) {
     // paired waves (workgroup-shared event lists): two waves per workgroup
 #define CVR_WPAIR(E, M) reinterpret_cast<const void*>(&k_wpair<E, 5, M>)
@@ -1637,6 +1646,9 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
     void* args[] = {&mm, &ll};
     return hipLaunchKernel(fn, dim3(grid / 2), dim3(128), args, 0, s);
   }
+#else
+  if (pair) return hipErrorInvalidValue;  // (cvr_set_option refuses it first)
+#endif
   const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
                          : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush, uniform)
                                         : wpool_fn<false>(waves, sparse, full, flush, uniform));
@@ -1646,6 +1658,8 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   void* args[] = {&mm, &ll};
   return hipLaunchKernel(fn, dim3(grid), dim3(64), args, 0, s);
 }
+
+bool wpool_pair_built() { return CVR_WPOOL_PAIR != 0; }
 
 uint32_t wpool_slots(int waves, bool sparse) {
   constexpr int kEmB = CVR_WPOOL_EMASK ? 4 * kEmaskWords : 0;

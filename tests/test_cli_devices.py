@@ -94,12 +94,40 @@ def test_cli_ragged_tiles_leave_remainder_black(cvr, tmp_path):
     assert_pixels_close(img1, reference_image(cvr, "bucky", 100, 70, (1, 1), 2), 2, "fallback single device")
 
 
-def test_cli_rejects_bad_devices(tmp_path):
-    """Host-only: an empty --devices list is a usage error (exit 2) before any
-    scene or device is touched."""
-    r = subprocess.run([CLI, "--synthetic", "bucky", "--devices", "0", "--interactive", "0", "-o",
+@pytest.mark.parametrize("devices", ["0", "1,", ",1", "a,b", "0,,1", "2x", "-1,0"])
+def test_cli_rejects_bad_devices(tmp_path, devices):
+    """Host-only: a zero count, an empty entry or a non-numeric one is a usage error
+    (exit 2) before any scene or device is touched (not silently device 0)."""
+    r = subprocess.run([CLI, "--synthetic", "bucky", "--devices", devices, "--interactive", "0", "-o",
                         str(tmp_path / "x")], capture_output=True, text=True, timeout=60)
-    assert r.returncode == 2 and "--devices" in r.stderr
+    assert r.returncode == 2 and "--devices" in r.stderr, (devices, r.returncode, r.stderr)
+
+
+@pytest.mark.gpu
+def test_cli_thread_binding_does_not_block_shard(cvr, tmp_path):
+    """--rng-binding thread has no 8x8-block work order: the CLI renders on one
+    device instead of writing part-sums of other pixels (round-5 advisor), and the
+    library refuses such a block-shard share outright."""
+    W, H, iters = 64, 64, 2
+    img, out = run_cli(tmp_path, "thr", "--synthetic", "bucky", "-r", str(W), str(H), "-i", str(iters),
+                       "--rng-binding", "thread", "--devices", "0,0")
+    assert "rendering on device 0" in out and "block shards of the image" not in out
+    assert np.isfinite(img).any() and img.max() > 0
+    scene = cvr.Scene.synthetic("bucky")
+    c = cvr.Context(0, "regenerationSK")
+    c.set_medium(scene.medium)
+    iv, r2v = cvr.default_camera(W, H)
+    c.set_camera(iv, r2v, (W, H))
+    c.set_option(cvr.OPT_RNG_BINDING, 1)
+    c.init()
+    c.set_block_shard(0, 2)
+    pim = cvr.PinnedImage(W, H)
+    try:
+        with pytest.raises(RuntimeError, match="UNSUPPORTED"):
+            c.render_share_to_host(pim.ptr.value, pim.floats, W, H, (1, 1), iters)
+    finally:
+        pim.close()
+        c.close()
 
 
 @pytest.mark.gpu

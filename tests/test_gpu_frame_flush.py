@@ -64,7 +64,7 @@ def test_flush_equals_copy_and_oracle(cvr, oracle_mod, name, res, iters):
     try:
         buf.img[:] = np.nan
         c.set_seed(0)
-        _, st = c.render_frame(buf.ptr.value, 1)
+        _, st = c.render_frame(buf.ptr.value, 1, host_floats=buf.img.size)
         blocks, fallbacks = c.frame_flush_info()
         assert (blocks, fallbacks) == ((w // 8) * (h // 8), 0)
         assert c.get_seed() == w * h * iters  # reset() as the copy path advances it
@@ -74,7 +74,7 @@ def test_flush_equals_copy_and_oracle(cvr, oracle_mod, name, res, iters):
         c.set_option(cvr.OPT_FRAME_FLUSH, 0)
         buf.img[:] = np.nan
         c.set_seed(0)
-        _, st0 = c.render_frame(buf.ptr.value, 1)
+        _, st0 = c.render_frame(buf.ptr.value, 1, host_floats=buf.img.size)
         assert c.frame_flush_info() == (0, 0)
         copied = buf.img.copy()
         for k in COUNTERS:
@@ -113,14 +113,14 @@ def test_flush_repeated_frames_and_bands(cvr):
         imgs = []
         for _ in range(3):
             c.set_seed(7)
-            c.render_frame(buf.ptr.value, 1, stats=False)
+            c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
             assert c.frame_flush_info() == (256, 0)
             imgs.append(buf.img.copy())
         for im in imgs[1:]:
             assert np.array_equal(im[..., 3], imgs[0][..., 3])
             assert_pixels_close(im[..., :3], imgs[0][..., :3], 3, "repeat")
         c.set_seed(7)
-        c.render_frame(buf.ptr.value, 2, stats=False)
+        c.render_frame(buf.ptr.value, 2, stats=False, host_floats=buf.img.size)
         assert c.frame_flush_info()[0] == 0
         assert_pixels_close(buf.img[..., :3], imgs[0][..., :3], 3, "two bands")
     finally:
@@ -130,7 +130,7 @@ def test_flush_repeated_frames_and_bands(cvr):
     buf = Pinned(100, 64)
     try:
         c.set_seed(0)
-        c.render_frame(buf.ptr.value, 1, stats=False)
+        c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
         assert c.frame_flush_info()[0] == 0
     finally:
         buf.close()
@@ -147,21 +147,21 @@ def test_flush_with_block_order_and_other_budgets(cvr):
     try:
         c.set_option(cvr.OPT_FRAME_FLUSH, 0)
         c.set_seed(3)
-        c.render_frame(buf.ptr.value, 1, stats=False)
+        c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
         ref = buf.img.copy()
         c.set_option(cvr.OPT_FRAME_FLUSH, 1)
         nb, _, _ = c.launch_blocks()
         c.set_block_order(np.random.default_rng(5).permutation(nb).astype(np.uint32))
         buf.img[:] = np.nan
         c.set_seed(3)
-        c.render_frame(buf.ptr.value, 1, stats=False)
+        c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
         assert c.frame_flush_info() == (256, 0)
         assert np.array_equal(buf.img[..., 3], ref[..., 3])
         assert_pixels_close(buf.img[..., :3], ref[..., :3], 3, "block order")
         c.set_option(cvr.OPT_WAVES, 4)
         buf.img[:] = np.nan
         c.set_seed(3)
-        c.render_frame(buf.ptr.value, 1, stats=False)
+        c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
         assert c.frame_flush_info()[0] == 0
         assert np.array_equal(buf.img[..., 3], ref[..., 3])
         assert_pixels_close(buf.img[..., :3], ref[..., :3], 3, "4 waves")
@@ -179,20 +179,20 @@ def test_flush_fallback_copy(cvr):
     buf = Pinned(96, 64)
     try:
         c.set_seed(1)
-        c.render_frame(buf.ptr.value, 1, stats=False)
+        c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
         assert c.frame_flush_info() == (96, 0)
         ref = buf.img.copy()
         c.set_option(cvr.OPT_FRAME_FLUSH, 2)
         buf.img[:] = np.nan
         c.set_seed(1)
-        _, st = c.render_frame(buf.ptr.value, 1)
+        _, st = c.render_frame(buf.ptr.value, 1, host_floats=buf.img.size)
         assert c.frame_flush_info() == (0, 1)
         assert st.paths == 96 * 64 * 3
         assert np.array_equal(buf.img[..., 3], ref[..., 3])
         assert_pixels_close(buf.img[..., :3], ref[..., :3], 3, "fallback")
         c.set_option(cvr.OPT_FRAME_FLUSH, 1)
         c.set_seed(1)
-        c.render_frame(buf.ptr.value, 1, stats=False)
+        c.render_frame(buf.ptr.value, 1, stats=False, host_floats=buf.img.size)
         assert c.frame_flush_info() == (96, 1)
         assert_pixels_close(buf.img[..., :3], ref[..., :3], 3, "flush after fallback")
     finally:

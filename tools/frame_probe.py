@@ -49,12 +49,12 @@ def main():
             parts, flush = table[v]
             c.set_option(cvr.OPT_FRAME_FLUSH, flush)
             for _ in range(3):
-                c.render_frame(host.data_ptr(), parts, stats=False)
+                c.render_frame(host.data_ptr(), parts, stats=False, host_floats=host.numel())
             t0 = time.perf_counter()
             for _ in range(a.reps):
-                c.render_frame(host.data_ptr(), parts, stats=False)
+                c.render_frame(host.data_ptr(), parts, stats=False, host_floats=host.numel())
             ms = (time.perf_counter() - t0) / a.reps * 1e3
-            _, st = c.render_frame(host.data_ptr(), parts)
+            _, st = c.render_frame(host.data_ptr(), parts, host_floats=host.numel())
             print(f"round {rnd} {v:6s}: {ms:.3f} ms per render (one more with counters: clear..end "
                   f"{st.kernel_ms:.3f} ms, flushed blocks {c.frame_flush_info()}), "
                   f"{W * H * a.iters / ms / 1e3:.1f} Msamples/s", flush=True)
