@@ -49,6 +49,22 @@
 #ifndef CVR_WPOOL_PAIR
 #define CVR_WPOOL_PAIR 0
 #endif
+// Diagnostic build (make variant NAME=tail DEFS=-DCVR_WPOOL_TAILSTAMP=1, tools/tail_wpool.py):
+// per wave, s_memrealtime at its start, when it first finds every queue exhausted and at its
+// end, with its live paths and event batches after that point.
+#ifndef CVR_WPOOL_TAILSTAMP
+#define CVR_WPOOL_TAILSTAMP 0
+#endif
+// The drain's wide track (round 6, wide_track): once every queue is exhausted and
+// at most 64 / CVR_WPOOL_WIDE paths are ready, each gets CVR_WPOOL_WIDE lanes that
+// evaluate its next CVR_WPOOL_WIDE tentative points at once.  0: off, the default:
+// bit-exact but no faster (K 16 / 8 / 4: one render at a time +0.1-0.3%, the 1/8
+// block shard +1%, renders in flight -0.5-1%; profiles/round6/ab/wide_drain_ab.log),
+// since half of a draining wave's time is its event batches, which stay one lane
+// per path (profiles/round6/tail_c2_stamps.log).
+#ifndef CVR_WPOOL_WIDE
+#define CVR_WPOOL_WIDE 0
+#endif
 #ifndef CVR_WPOOL_LOOK
 #define CVR_WPOOL_LOOK 2
 #endif
@@ -468,6 +484,102 @@ __device__ void frame_flusher(const LaunchParams& L) {
   if (lane == 0) __hip_atomic_store(F.status + f, stored, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---- the launch's drain: one path's Woodcock points across K lanes -----------
+// Once every queue is exhausted a wave's pool only drains: fewer paths than lanes
+// are left, and the last ones run one segment at a time, each Woodcock group a
+// dependent brick-word load (round-6 tail stamps, tools/tail_wpool.py: half of a
+// draining wave's time is its track loop).  The points of a segment depend on
+// nothing but its RNG stream, so with few paths left each ready path gets K
+// lanes (one group of a DPP row): lane p of the group takes the path's draws
+// 2p + 1 and 2p + 2 (every lane steps the XORWOW sequence up to its own pair),
+// the distances follow the sequential chain t_p = fma(-log xi_p, inv_sigma,
+// t_{p-1}) in order (one row shift per point), and all K brick words (and the
+// cells the bounds do not settle) load at once.  The first point of the group
+// that ends the segment (past max_t, or a real collision) is found by a ballot;
+// the points after it are dropped, as in the two-point lookahead, and the path's
+// t and RNG are that point's (its lane stores them into the slot).  The same
+// candidates in the same order: the same results, steps and fetch counts as one
+// point at a time (Utilities.cuh:147-152, tests/test_gpu_records.py).  On exit
+// lane 0 of each group holds its path's finished segment, filed by the next
+// swap.  Groups past `ngroups` repeat group 0's path and write nothing.
+template <int K, int kSlots, int kEm, class Pool>
+__device__ __forceinline__ void wide_track(Pool& S, const MediumParams& m, uint32_t lane, uint32_t ready_head,
+                                           uint32_t ngroups, int& slot, int& fst, V3& o, V3& d, Rng& rng,
+                                           float& t, float& max_t, uint32_t& c_steps, uint32_t& c_fetch) {
+  static_assert(K >= 2 && K <= 16 && (K & (K - 1)) == 0, "a group lies within one 16-lane DPP row");
+  constexpr uint32_t kGroupMask = K == 32 ? 0xFFFFFFFFu : (1u << K) - 1u;
+  // (through an empty asm: lane / K and lane % K are loop-invariant, and hoisted to the
+  // prologue they would hold two VGPRs across the track loop)
+  uint32_t ln = lane;
+  asm volatile("" : "+v"(ln));
+  const uint32_t g = ln / K, p = ln % K;
+  const bool real = g < ngroups;
+  const uint32_t r = ready_head + (real ? g : 0u);
+  const uint32_t s = S.ready[r >= (uint32_t)kSlots ? r - kSlots : r];
+  V3 go, gd;
+  Rng gr;
+  float gt, gmax;
+  load_track(S, s, go, gd, gr, gt, gmax);
+  int res = 0;        // the group's segment result once it ended: 1 past max_t, 2 accepted
+  bool open = real;   // group-uniform: the segment has not ended
+  for (;;) {
+    // lane p: draws 2p + 1, 2p + 2 of the group's stream (divergent loop, K rounds)
+    Rng lr = gr;
+    float xi = 0.0f, xt = 0.0f;
+    for (uint32_t i = 0; i <= p; ++i) {
+      xi = rng_float(lr);
+      xt = rng_float(lr);
+    }
+    const float a = -det_logf_normal(__builtin_fmaxf(xi, CVR_EPSILON_F));
+    // t_p = fma(a_p, inv_sigma, t_{p-1}) in order: woodcock_advance's chain, one row shift per point
+    float tp = det_fmaf(a, m.inv_sigma, gt);
+#pragma unroll
+    for (int j = 1; j < K; ++j) {
+      const float prev = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(tp), 0x111 /* row_shr:1 */,
+                                                                    0xF, 0xF, false));
+      const float tn = det_fmaf(a, m.inv_sigma, prev);
+      tp = p == (uint32_t)j ? tn : tp;
+    }
+    WoodcockPoint P;
+    if constexpr (kEm != 0)
+      P = woodcock_point_em<kEm>(m, go, gd, tp, S.em);
+    else
+      P = woodcock_point(m, go, gd, tp);
+    int rr = 0;
+    bool fetched = false;
+    if (!(tp <= gmax)) {
+      rr = 1;
+    } else if (!(P.qb < xt)) {
+      fetched = true;
+      const float rho = m.scale * woodcock_density(m, P);
+      if (!(rho * m.inv_sigma < xt)) rr = 2;
+    }
+    const unsigned long long me = __ballot(rr != 0), m1 = __ballot(rr == 1);
+    const uint32_t gb = (uint32_t)(me >> (g * K)) & kGroupMask;
+    const uint32_t end = gb ? (uint32_t)__builtin_ctz(gb) : (uint32_t)K;
+    if (open) {
+      c_fetch += (fetched && p <= end) ? 1u : 0u;
+      if (p == 0) c_steps += end < (uint32_t)K ? end + 1u : (uint32_t)K;
+      // the group's new track state: the ending point's, or the last point's
+      if (p == (end < (uint32_t)K ? end : (uint32_t)K - 1u)) store_track(S, s, tp, lr);
+      if (end < (uint32_t)K) {
+        res = ((m1 >> (g * K + end)) & 1ull) ? 1 : 2;
+        open = false;
+      }
+    }
+    if (__ballot(open) == 0ull) break;
+    if (open) {  // the next K points from the state just stored (one wave: LDS in order)
+      V3 o2, d2;
+      load_track(S, s, o2, d2, gr, gt, gmax);
+    }
+  }
+  if (real && p == 0) {
+    slot = (int)s;
+    fst = res;
+    load_track(S, s, o, d, rng, t, max_t);
+  }
+}
+
 }  // namespace
 
 // kMed: the medium layout the instance is compiled for (kMedDense any dense medium,
@@ -478,6 +590,10 @@ __device__ void frame_flusher(const LaunchParams& L) {
 // kFlush: the in-launch output instance (cvr_render_frame, CVR_OPT_FRAME_FLUSH);
 // the other instances carry none of its code.
 enum : int { kMedDense = 0, kMedSparse = 1, kMedDenseFull = 2, kMedDenseFullUniform = 3 };
+#if CVR_WPOOL_TAILSTAMP
+constexpr uint32_t kTailWaves = 16384;
+__device__ unsigned long long g_tail[8 * kTailWaves];
+#endif
 // kMedMK (or-ed into kMed): naiveMK's walk (NaiveVolPTmk_kernel.cuh:20-151) on the wave
 // pool, round 5: a new path runs d_init (camera ray on the (iteration, pixel, 0) stream,
 // AABB, the GGX sample at the box, Q12) and every segment starts as d_extend does, with
@@ -525,6 +641,11 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     __builtin_assume(m.sbounds != nullptr);
     m.albedo_uniform = 0u;
   }
+#if CVR_WPOOL_TAILSTAMP
+  const unsigned long long ts_start = __builtin_amdgcn_s_memrealtime();
+  unsigned long long ts_ex = 0, ts_ev = 0, ts_a = 0;
+  uint32_t ts_live = 0, ts_batches = 0, ts_trk = 0, ts_steps0 = 0, ts_seg0 = 0;
+#endif
   static_assert(sizeof(WavePool<kSlots, kEm>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
                 "wave pool exceeds the LDS budget of kWaves waves per SIMD");
   static_assert(kSlots <= 256, "the pool's rings and stacks hold slot indices as uint8_t");
@@ -584,6 +705,17 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     float t = 0.0f, max_t = 0.0f;
     const float4* pcp = nullptr;  // kLookDefer: the pending fetch's cell and test value
     float pxt = 0.0f;
+    if constexpr (CVR_WPOOL_WIDE != 0) {
+      // the drain (every queue exhausted) with at most 64 / K paths ready: K lanes per path
+      // (wide_track); the segments end there and the first swap below files them
+      if (n_ready != 0u && n_ready <= 64u / CVR_WPOOL_WIDE && (S.cur[2] & kCurExhausted)) {
+        wide_track<CVR_WPOOL_WIDE, kSlots, kEm>(S, m, lane, ready_head, n_ready, slot, fst, o, d, rng, t, max_t,
+                                                c_steps, c_fetch);
+        ready_head += n_ready;
+        if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
+        n_ready = 0;
+      }
+    }
     for (;;) {
       const unsigned long long trk = (__ballot(slot >= 0) & __ballot(fst == 0));
       const uint32_t n_trk = (uint32_t)__popcll(trk);
@@ -747,6 +879,9 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 
     // ================================================= EVENT ==============
     __builtin_amdgcn_s_setprio(kPrioEvent);
+#if CVR_WPOOL_TAILSTAMP
+    if (ts_ex != 0) ts_a = __builtin_amdgcn_s_memrealtime();
+#endif
     if constexpr (kFlush) {
       const uint32_t pend = S.pend;  // the last batch's ended paths (in-launch output)
       if (pend != 0u) {
@@ -1031,6 +1166,17 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     }
     if (S.cur[2] & kCurExhausted) {
       const uint32_t n_live = n_ready + n_lb + n_lc;
+#if CVR_WPOOL_TAILSTAMP
+      if (ts_ex == 0) {
+        ts_ex = __builtin_amdgcn_s_memrealtime();
+        ts_live = n_live;
+        ts_steps0 = c_steps;
+        ts_seg0 = S.cnt[STAT_SEGMENTS];
+      } else {
+        ts_ev += __builtin_amdgcn_s_memrealtime() - ts_a;
+      }
+      ++ts_batches;
+#endif
       // The launch's drain.  A wave's lanes cannot all be busy any more, and
       // a batch that waits for its slowest segment stretches the last paths'
       // lives: the batch should run once drain x waiting >= tracking paths.
@@ -1047,6 +1193,26 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     }
   }
 
+#if CVR_WPOOL_TAILSTAMP
+  {
+    const unsigned long long ts_end = __builtin_amdgcn_s_memrealtime();
+    uint32_t dsteps = c_steps - ts_steps0;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) dsteps += __shfl_xor(dsteps, off);
+    if (lane == 0 && blockIdx.x < kTailWaves) {
+      const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
+      unsigned long long* g = g_tail + 8 * blockIdx.x;
+      g[0] = ts_start;
+      g[1] = ts_ex;
+      g[2] = ts_end;
+      g[3] = (unsigned long long)ts_live | (unsigned long long)ts_batches << 16 | (unsigned long long)xcc << 40;
+      g[4] = ts_ev;
+      g[5] = dsteps;
+      g[6] = S.cnt[STAT_SEGMENTS] - ts_seg0;
+      g[7] = ts_trk;
+    }
+  }
+#endif
   if constexpr (kFlush) {
     const uint32_t pend = S.pend;  // raw: the last batch's ended paths
     if (pend != 0u) {
@@ -1660,6 +1826,19 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
 }
 
 bool wpool_pair_built() { return CVR_WPOOL_PAIR != 0; }
+
+#if CVR_WPOOL_TAILSTAMP
+// (diagnostic build) the per-wave stamps of the last launch, 8 u64 per wave
+extern "C" int cvr_debug_tailstamps(unsigned long long* host, size_t n_waves) {
+  if (n_waves > kTailWaves) n_waves = kTailWaves;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tail), n_waves * 64, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+extern "C" int cvr_debug_tailstamps_clear() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_tail)) != hipSuccess) return -2;
+  return hipMemset(p, 0, sizeof(unsigned long long) * 8 * kTailWaves) == hipSuccess ? 0 : -2;
+}
+#endif
 
 uint32_t wpool_slots(int waves, bool sparse) {
   constexpr int kEmB = CVR_WPOOL_EMASK ? 4 * kEmaskWords : 0;
