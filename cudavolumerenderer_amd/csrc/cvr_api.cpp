@@ -267,13 +267,16 @@ bool mk_on_wpool(const cvr_ctx* c) {
 // ms per render, profiles/round2/overlap_small_shards.log; round 4, three in
 // flight: 1/4 shard 1.282 vs 1.320 ms, 1/8 shard 0.724 vs 0.768 at 3/4 grid,
 // profiles/round4/shard_grid.log); alone the full grid is faster.
+// The grid counts waves, in whole workgroups of the instance (cvr::wpool_wpg).
 uint32_t wpool_launch_grid(const cvr_ctx* c, uint64_t n_paths) {
-  if (c->grid_override) return c->grid_override;
+  const uint32_t wpg = cvr::wpool_wpg(wpool_waves_for(c, c->m.leaves != nullptr), c->m.leaves != nullptr);
+  auto whole = [wpg](uint32_t g) { return std::max(wpg, g / wpg * wpg); };
+  if (c->grid_override) return whole(c->grid_override);
   const uint32_t full = (uint32_t)(c->m.leaves ? c->wpool_grid_sparse : c->wpool_grid);
   const uint32_t half = std::max(1u, full / 2), quarter = std::max(1u, full / 4);
-  if (n_paths < 64ull * full) return c->inflight > 1 ? quarter : half;
-  if (c->inflight > 1 && n_paths < 2048ull * full) return half;
-  return full;
+  if (n_paths < 64ull * full) return whole(c->inflight > 1 ? quarter : half);
+  if (c->inflight > 1 && n_paths < 2048ull * full) return whole(half);
+  return whole(full);
 }
 
 int ensure_device(cvr_ctx* c) {

@@ -59,10 +59,15 @@ bool wpool_pair_built();
 // naive_mk: naiveMK's walk on the wave pool (5 waves per SIMD, no records / in-launch output).
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
                         hipStream_t s, bool pair = false, bool naive_mk = false);
-hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu);
+// Resident waves per CU of the wave-pool instance (workgroups per CU x waves per workgroup).
+hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* waves_per_cu);
 // Pool slots per wave of the wave-pool kernel instance (LaunchParams::pool_T
 // needs grid * slots float4).
 uint32_t wpool_slots(int waves, bool sparse);
+// Waves per workgroup of the wave-pool instance: 1 for dense media; sparse media run
+// several wave-private pools per workgroup that share one LDS copy of the launch
+// parameters and the empty-region mask.  A wave-pool grid (in waves) is a multiple.
+uint32_t wpool_wpg(int waves, bool sparse);
 // regenerationSK with the RNG bound to the persistent thread (CVR_OPT_RNG_BINDING 1):
 // `grid` one-wave workgroups, path ids from the launch's single queue head.
 hipError_t launch_regen_thread(const MediumParams& m, const LaunchParams& L, bool scatter_eps, uint32_t grid,

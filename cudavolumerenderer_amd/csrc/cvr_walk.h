@@ -184,7 +184,16 @@ struct MediumParams {
   const uint32_t* emask;
   uint32_t eshift, eshy, eshz;
 };
-constexpr int kEmaskWords = 64;
+// Words of the empty-region mask (a power of two): 64 (2048 super-bricks, C5's
+// cloud at 128^3 cells each), staged once per workgroup of the sparse instances,
+// whose workgroups hold four wave-private pools (cvr_wpool.hip, kWpgSparse).  A
+// finer mask costs the pools slots: 512 words (64^3 cells, 27% fewer word loads
+// on C5) ran 114.4 ms against 112.9 with 64 (profiles/round6/ab/c5_wpg_mask_ab.log).
+#ifndef CVR_WPOOL_EMASK_WORDS
+#define CVR_WPOOL_EMASK_WORDS 64
+#endif
+constexpr int kEmaskWords = CVR_WPOOL_EMASK_WORDS;
+static_assert(kEmaskWords >= 64 && (kEmaskWords & (kEmaskWords - 1)) == 0, "mask words: a power of two >= 64");
 
 // Brick-bound code -> bound (MediumParams::bounds): the float with bits
 // (c << 19) + (112 << 23), one v_lshl_add_u32.  c = 16 e + m stands for

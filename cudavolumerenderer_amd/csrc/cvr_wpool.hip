@@ -37,6 +37,17 @@
 #ifndef CVR_WPOOL_EMASK
 #define CVR_WPOOL_EMASK 1
 #endif
+// Waves per workgroup of the sparse instances (round 6): each wave keeps its own
+// pool, and the workgroup stages the launch parameters and the empty-region mask
+// (kEmaskWords words) once for all of them, so a finer mask costs each wave
+// 1/kWpg of its LDS.  1: one wave per workgroup (every dense instance).
+#ifndef CVR_WPOOL_SPARSE_WPG
+#define CVR_WPOOL_SPARSE_WPG 4
+#endif
+// The same for the dense instances (experiment: 1 is one wave per workgroup).
+#ifndef CVR_WPOOL_DENSE_WPG
+#define CVR_WPOOL_DENSE_WPG 1
+#endif
 // Tentative points per lane per Woodcock group (the lookahead below).  The
 // track loop runs CVR_WPOOL_UNROLL / kLook groups between swap checks.
 // Sparse instances: a point that needs its cell parks until the end of the track
@@ -104,14 +115,24 @@ __device__ __forceinline__ float opaque_s(float x) {
 // although the occupancy API answers 20 for all of them; 10240 B fit 16).  A
 // budget of 163840 / 20 = 8192 B therefore ran 4.5 waves per SIMD, not 5.
 constexpr int kLdsGranule = 1280;
-template <int kWaves, int kExtra = 0>
+template <int kWaves, int kExtra = 0, int kWpg = 1>
 struct PoolSize {
-  // LDS bytes per one-wave workgroup (kExtra: bytes of it not for slots)
-  static constexpr int kBudget = 163840 / (4 * kWaves) / kLdsGranule * kLdsGranule;
+  static_assert((4 * kWaves) % kWpg == 0, "a CU's waves split into whole workgroups");
+  // LDS bytes per workgroup of kWpg waves (kExtra: bytes of it shared by its waves,
+  // besides the launch parameters)
+  static constexpr int kBudget = 163840 / (4 * kWaves / kWpg) / kLdsGranule * kLdsGranule;
   static constexpr int kParams = (int)((sizeof(LaunchParams) + 15) / 16 * 16);
-  static constexpr int value = (kBudget - kParams - 24 - 4 * STAT_COUNT - kExtra) / 64;
+  static constexpr int value = ((kBudget - kParams - kExtra) / kWpg - 24 - 4 * STAT_COUNT) / 64;
   static_assert(4 * STAT_COUNT + 8 + 12 + 4 <= 4 * STAT_COUNT + 24, "pool header exceeds its LDS reserve");
 };
+constexpr int kWpgSparse = CVR_WPOOL_SPARSE_WPG, kWpgDense = CVR_WPOOL_DENSE_WPG;
+// waves per workgroup of an instance (kMedMk's low bits: the medium layout): kWpgSparse
+// on sparse media (kWpgDense on dense ones) when a CU's 4 kWaves waves split into such
+// workgroups, else 4 (sparse) or 1 (dense)
+constexpr int wpg_of(int kMedMk, int kWaves) {
+  return (kMedMk & 3) != 1 /* kMedSparse */ ? ((4 * kWaves) % kWpgDense == 0 ? kWpgDense : 1)
+                                            : ((4 * kWaves) % kWpgSparse == 0 ? kWpgSparse : 4);
+}
 // Sparse media (C5) split the slot too and run 5 waves per SIMD: 142.7 ms vs
 // 147.6 with the event part in LDS at 4 waves (round 3, once the global part's
 // loads and stores stopped being flat instructions that LDS waits also waited
@@ -127,15 +148,10 @@ struct PoolSize {
 // the pool holds 30% more paths, enough for 5 waves per SIMD (C2: 5.25 ms
 // vs 5.40 at 4 waves with the whole slot in LDS).
 // Sparse instances also stage the medium's empty-region mask (MediumParams::
-// emask, kEm words; CVR_WPOOL_EMASK): 4 slots' worth of LDS.
-template <int kEm>
-struct EmPart {
-  uint32_t em[kEm];
-};
-template <>
-struct EmPart<0> {};
-template <int kSlots, int kEm = 0>
-struct WavePool : EmPart<kEm> {
+// emask, kEmaskWords words; CVR_WPOOL_EMASK), once per workgroup beside the
+// launch parameters (k_wpool's EM).
+template <int kSlots>
+struct WavePool {
   float4 a[kSlots], b[kSlots];
   uint4 c[kSlots];
   uint2 e[kSlots];
@@ -301,15 +317,15 @@ __device__ __forceinline__ void splat_wave(Pool& S, const LaunchParams& L, const
 // Debug records (LaunchParams::rec): a path's final state when it ends, in
 // the oracle's per-path record layout (cvr_kernels.h PathRecord; steps and
 // density counts are per lane here, so they stay 0).
-template <int kSlots>
-__device__ __forceinline__ uint32_t* rec_pids(const LaunchParams& L) {
-  // the path-id array (grid * slots u32) sits just below the records
-  return reinterpret_cast<uint32_t*>(L.rec) - (size_t)gridDim.x * kSlots + (size_t)blockIdx.x * kSlots;
+template <int kSlots, int kWpg>
+__device__ __forceinline__ uint32_t* rec_pids(const LaunchParams& L, uint32_t gw) {
+  // the path-id array (grid * slots u32, grid in waves) sits just below the records
+  return reinterpret_cast<uint32_t*>(L.rec) - (size_t)gridDim.x * kWpg * kSlots + (size_t)gw * kSlots;
 }
-template <int kSlots>
-__device__ __forceinline__ void record_end(const LaunchParams& L, uint32_t s, const PathState& ps, uint32_t flags,
-                                           uint32_t nseg) {
-  const uint32_t pid = rec_pids<kSlots>(L)[s];
+template <int kSlots, int kWpg>
+__device__ __forceinline__ void record_end(const LaunchParams& L, uint32_t gw, uint32_t s, const PathState& ps,
+                                           uint32_t flags, uint32_t nseg) {
+  const uint32_t pid = rec_pids<kSlots, kWpg>(L, gw)[s];
   PathRecord r = {};
   r.image_id = ps.image_id;
   r.flags = flags;
@@ -424,9 +440,8 @@ __device__ __forceinline__ void store_blocks(const LaunchParams& L, const FrameF
 // copies the image after the launch.
 constexpr unsigned long long kFlushPatience = 100000000ull;  // s_memrealtime ticks (100 MHz)
 constexpr unsigned int kFlushed = 0x80000000u;
-__device__ void frame_flusher(const LaunchParams& L) {
+__device__ void frame_flusher(const LaunchParams& L, uint32_t f, uint32_t lane) {
   const FrameFlush F = *frame_header(L.frame_done);
-  const uint32_t lane = threadIdx.x, f = blockIdx.x;
   if (F.give_up) {  // test mode: exercise the host's fallback copy
     if (lane == 0) __hip_atomic_store(F.status + kFrameFlushers, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
@@ -502,8 +517,9 @@ __device__ void frame_flusher(const LaunchParams& L) {
 // point at a time (Utilities.cuh:147-152, tests/test_gpu_records.py).  On exit
 // lane 0 of each group holds its path's finished segment, filed by the next
 // swap.  Groups past `ngroups` repeat group 0's path and write nothing.
-template <int K, int kSlots, int kEm, class Pool>
-__device__ __forceinline__ void wide_track(Pool& S, const MediumParams& m, uint32_t lane, uint32_t ready_head,
+template <int K, int kSlots, int kEm, class Pool, class EmWords>
+__device__ __forceinline__ void wide_track(Pool& S, const EmWords& em, const MediumParams& m, uint32_t lane,
+                                           uint32_t ready_head,
                                            uint32_t ngroups, int& slot, int& fst, V3& o, V3& d, Rng& rng,
                                            float& t, float& max_t, uint32_t& c_steps, uint32_t& c_fetch) {
   static_assert(K >= 2 && K <= 16 && (K & (K - 1)) == 0, "a group lies within one 16-lane DPP row");
@@ -542,7 +558,7 @@ __device__ __forceinline__ void wide_track(Pool& S, const MediumParams& m, uint3
     }
     WoodcockPoint P;
     if constexpr (kEm != 0)
-      P = woodcock_point_em<kEm>(m, go, gd, tp, S.em);
+      P = woodcock_point_em<kEm>(m, go, gd, tp, em);
     else
       P = woodcock_point(m, go, gd, tp);
     int rr = 0;
@@ -601,7 +617,7 @@ __device__ unsigned long long g_tail[8 * kTailWaves];
 // event-only word holds the path id (iteration and pixel) instead of the pixel.
 constexpr int kMedMK = 4;
 template <bool kScatterEps, int kWaves, int kMedMk, bool kRecord, bool kFlush>
-__global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
+__global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr bool kMK = (kMedMk & kMedMK) != 0;
   constexpr int kMed = kMedMk & 3;
   static_assert(!kMK || (kScatterEps && !kRecord && !kFlush), "naiveMK: scatter -eps, no records / in-launch output");
@@ -611,15 +627,21 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   constexpr bool kLookDefer = kSparse && CVR_WPOOL_SPARSE_DEFER;
   // (dense media: +7% C2, +6% C3 with a 16-word mask)
   constexpr int kEm = kSparse && CVR_WPOOL_EMASK ? kEmaskWords : 0;
-  constexpr int kSlots = PoolSize<kWaves, 4 * kEm>::value;
-  // Dense instances see the sparse pointers as constant null, so the sparse
-  // branches of the walk code fold away and take no scalar registers.
-  if constexpr (kFlush) {
+  // waves per workgroup, each with a pool of its own (kWpgSparse on sparse media)
+  constexpr int kWpg = wpg_of(kMedMk, kWaves);
+  constexpr int kSlots = PoolSize<kWaves, 4 * kEm, kWpg>::value;
+  if constexpr (kFlush && kWpg == 1) {
     if (Lk.frame_done != nullptr && blockIdx.x < kFrameFlushers) {
-      frame_flusher(Lk);
+      frame_flusher(Lk, blockIdx.x, threadIdx.x);
       return;
     }
   }
+  // the wave's index within its workgroup and within the launch (pool_T rows,
+  // records, home sub-queue): one-wave workgroups number as before
+  const uint32_t wv = kWpg > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0u;
+  const uint32_t gw = blockIdx.x * (uint32_t)kWpg + wv;
+  // Dense instances see the sparse pointers as constant null, so the sparse
+  // branches of the walk code fold away and take no scalar registers.
   MediumParams m = mk;
   if constexpr (!kSparse) {
     m.leaves = nullptr;
@@ -646,21 +668,31 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
   unsigned long long ts_ex = 0, ts_ev = 0, ts_a = 0;
   uint32_t ts_live = 0, ts_batches = 0, ts_trk = 0, ts_steps0 = 0, ts_seg0 = 0;
 #endif
-  static_assert(sizeof(WavePool<kSlots, kEm>) + sizeof(LaunchParams) <= (size_t)PoolSize<kWaves>::kBudget,
-                "wave pool exceeds the LDS budget of kWaves waves per SIMD");
+  static_assert(kWpg * sizeof(WavePool<kSlots>) + 4 * kEm + sizeof(LaunchParams) <=
+                    (size_t)PoolSize<kWaves, 0, kWpg>::kBudget,
+                "wave pools exceed the LDS budget of kWaves waves per SIMD");
   static_assert(kSlots <= 256, "the pool's rings and stacks hold slot indices as uint8_t");
-  __shared__ WavePool<kSlots, kEm> S;
+  __shared__ WavePool<kSlots> Sw[kWpg];
+  WavePool<kSlots>& S = Sw[wv];
+  // the empty-region mask (sparse media), one copy per workgroup
+  __shared__ uint32_t EM[kEm ? kEm : 1];
   // The launch parameters live in LDS: only the event code reads them, and
   // keeping them in SGPRs for the whole kernel spills the step loop's
   // scalars (v_readlane reloads in every Woodcock step).
   __shared__ LaunchParams L;
-  const uint32_t lane = threadIdx.x;
-  if (lane == 0) L = Lk;
+  const uint32_t lane = kWpg > 1 ? threadIdx.x & 63u : threadIdx.x;
+  if (threadIdx.x == 0) L = Lk;
   if constexpr (kEm != 0) {
-    static_assert(kEm == 64, "one mask word per lane");
-    S.em[lane] = m.emask ? m.emask[lane] : ~0u;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kEm; i += 64u * kWpg) EM[i] = m.emask ? m.emask[i] : ~0u;
   }
   __syncthreads();
+  // (a multi-wave workgroup's flushers take part in the barrier above)
+  if constexpr (kFlush && kWpg > 1) {
+    if (Lk.frame_done != nullptr && gw < kFrameFlushers) {
+      frame_flusher(Lk, gw, lane);
+      return;
+    }
+  }
   // Counters.  Event counts are popcounts of ballots that lane 0 adds to the
   // pool's LDS counters once per batch (no per-lane registers, no SGPRs, live
   // across the track loop); the track loop counts steps and fetches per lane.
@@ -671,12 +703,12 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     S.pend = 0u;
   }
   uint32_t n_over = 0;  // wave-uniform: segments whose last Woodcock step passed max_t
-  // home queue: the XCD's band, and within it sub-queue (workgroup / 8) mod sub
-  // (workgroups are dealt round-robin over the 8 XCDs)
+  // home queue: the XCD's band, and within it sub-queue (the wave's number among
+  // its XCD's waves) mod sub (workgroups are dealt round-robin over the 8 XCDs)
   if (lane == 0) {
     S.cur[0] = S.cur[1] = 0u;
     S.cur[2] = (((__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) % (L.n_queues / L.sub)) * L.sub +
-                (blockIdx.x >> 3) % L.sub)
+                ((blockIdx.x >> 3) * (uint32_t)kWpg + wv) % L.sub)
                << 8;
   }
   const uint32_t batch = L.batch;  // TRACK: swap finished segments once this many lanes are idle
@@ -709,7 +741,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       // the drain (every queue exhausted) with at most 64 / K paths ready: K lanes per path
       // (wide_track); the segments end there and the first swap below files them
       if (n_ready != 0u && n_ready <= 64u / CVR_WPOOL_WIDE && (S.cur[2] & kCurExhausted)) {
-        wide_track<CVR_WPOOL_WIDE, kSlots, kEm>(S, m, lane, ready_head, n_ready, slot, fst, o, d, rng, t, max_t,
+        wide_track<CVR_WPOOL_WIDE, kSlots, kEm>(S, EM, m, lane, ready_head, n_ready, slot, fst, o, d, rng, t, max_t,
                                                 c_steps, c_fetch);
         ready_head += n_ready;
         if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
@@ -804,7 +836,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
 #pragma unroll
           for (int k = 0; k < kLook; ++k) {
             if constexpr (kEm != 0)
-              Pk[k] = woodcock_point_em<kEm>(m, o, d, tk[k], S.em);
+              Pk[k] = woodcock_point_em<kEm>(m, o, d, tk[k], EM);
             else
               Pk[k] = woodcock_point(m, o, d, tk[k]);
           }
@@ -1016,7 +1048,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             } else {
               path_begin(L, pid, ps);
             }
-            if (kRecord) rec_pids<kSlots>(L)[s] = pid;
+            if (kRecord) rec_pids<kSlots, kWpg>(L, gw)[s] = pid;
             is.normal = mk3(0, 0, 0);
             nseg = 0;
             got = true;
@@ -1055,7 +1087,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             truncated = true;
             to_ln = true;
             if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
-            if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);
+            if (kRecord) record_end<kSlots, kWpg>(L, gw, s, ps, 2u, nseg);
           } else {
             ++nseg;
             seg_first = true;
@@ -1063,9 +1095,9 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
               escaped = true;  // splat below (splat_wave)
               to_ln = true;
               if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
-              if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
+              if (kRecord) record_end<kSlots, kWpg>(L, gw, s, ps, 1u, nseg);
             } else if (is.inside) {
-              store_full(S, L.pool_T + (size_t)blockIdx.x * kSlots, s, ps, is, nseg, ps.image_id);
+              store_full(S, L.pool_T + (size_t)(kWpg > 1 ? gw : blockIdx.x) * kSlots, s, ps, is, nseg, ps.image_id);
               to_ready = true;
             } else {
               kind = K_BOUNDARY;  // enters the box: boundary event in this batch
@@ -1073,7 +1105,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           }
         }
       }
-      float4* __restrict__ gT = L.pool_T + (size_t)blockIdx.x * kSlots;  // this wave's event-only slot part
+      float4* __restrict__ gT = L.pool_T + (size_t)(kWpg > 1 ? gw : blockIdx.x) * kSlots;  // this wave's event-only slot part
       if (lane < tb + tc) {
         load_full(S, gT, s, ps, is, nseg, t_hit);
         if constexpr (kMK) {  // the event-only word is the path id
@@ -1095,7 +1127,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
       if ((kind == K_BOUNDARY || kind == K_COLLIDE) && !alive) {  // the path died in roulette
         to_ln = true;
         if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
-        if (kRecord) record_end<kSlots>(L, s, ps, 0u, nseg);
+        if (kRecord) record_end<kSlots, kWpg>(L, gw, s, ps, 0u, nseg);
       }
       // ---- next segment: AABB test of the survivors ----------------------
       if (alive) {
@@ -1103,7 +1135,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
           truncated = true;
           to_ln = true;
           if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
-          if (kRecord) record_end<kSlots>(L, s, ps, 2u, nseg);
+          if (kRecord) record_end<kSlots, kWpg>(L, gw, s, ps, 2u, nseg);
         } else {
           ++nseg;
           seg_next = true;
@@ -1123,7 +1155,7 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
             escaped = true;  // splat below (splat_wave)
             to_ln = true;
             if (kFlush) S.meta[s] = ps.image_id;  // the ended path's pixel (in-launch output)
-            if (kRecord) record_end<kSlots>(L, s, ps, 1u, nseg);
+            if (kRecord) record_end<kSlots, kWpg>(L, gw, s, ps, 1u, nseg);
           } else {
             store_full(S, gT, s, ps, is, nseg, kMK ? mk_pid : ps.image_id);
             to_ready = is.inside;  // medium: Woodcock from t = 0
@@ -1199,9 +1231,9 @@ __global__ __launch_bounds__(64, kWaves) void k_wpool(MediumParams mk, LaunchPar
     uint32_t dsteps = c_steps - ts_steps0;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) dsteps += __shfl_xor(dsteps, off);
-    if (lane == 0 && blockIdx.x < kTailWaves) {
+    if (lane == 0 && gw < kTailWaves) {
       const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;
-      unsigned long long* g = g_tail + 8 * blockIdx.x;
+      unsigned long long* g = g_tail + 8 * gw;
       g[0] = ts_start;
       g[1] = ts_ex;
       g[2] = ts_end;
@@ -1795,10 +1827,12 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   if (L.rec && flush) return hipErrorInvalidValue;
   if (naive_mk) {
     if (waves != 5 || flush || L.rec) return hipErrorInvalidValue;
+    if (grid % wpool_wpg(waves, sparse)) return hipErrorInvalidValue;
     MediumParams mm = m;
     LaunchParams ll = L;
     void* args[] = {&mm, &ll};
-    return hipLaunchKernel(wpool_mk_fn(sparse, full, uniform), dim3(grid), dim3(64), args, 0, s);
+    return hipLaunchKernel(wpool_mk_fn(sparse, full, uniform), dim3(grid / wpool_wpg(waves, sparse)),
+                           dim3(64 * wpool_wpg(waves, sparse)), args, 0, s);
   }
 #if CVR_WPOOL_PAIR
   if (pair && waves == 5 && full && !flush && !L.rec && grid >= 2) {
@@ -1819,10 +1853,12 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
                          : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush, uniform)
                                         : wpool_fn<false>(waves, sparse, full, flush, uniform));
   if (!fn) return hipErrorInvalidValue;  // no record / in-launch output instance for this register budget
+  // (a grid of whole workgroups: pool_T and the record ids are sized for grid waves)
+  if (grid % wpool_wpg(waves, sparse)) return hipErrorInvalidValue;
   MediumParams mm = m;
   LaunchParams ll = L;
   void* args[] = {&mm, &ll};
-  return hipLaunchKernel(fn, dim3(grid), dim3(64), args, 0, s);
+  return hipLaunchKernel(fn, dim3(grid / wpool_wpg(waves, sparse)), dim3(64 * wpool_wpg(waves, sparse)), args, 0, s);
 }
 
 bool wpool_pair_built() { return CVR_WPOOL_PAIR != 0; }
@@ -1840,18 +1876,24 @@ extern "C" int cvr_debug_tailstamps_clear() {
 }
 #endif
 
+uint32_t wpool_wpg(int waves, bool sparse) { return (uint32_t)wpg_of(sparse ? kMedSparse : kMedDense, waves); }
+
 uint32_t wpool_slots(int waves, bool sparse) {
   constexpr int kEmB = CVR_WPOOL_EMASK ? 4 * kEmaskWords : 0;
-  if (sparse) return waves == 5 ? PoolSize<5, kEmB>::value : PoolSize<4, kEmB>::value;
-  return waves == 5   ? PoolSize<5>::value
-         : waves == 6 ? PoolSize<6>::value
-         : waves == 3 ? PoolSize<3>::value
-                      : PoolSize<4>::value;
+  if (sparse)
+    return waves == 5 ? PoolSize<5, kEmB, wpg_of(kMedSparse, 5)>::value : PoolSize<4, kEmB, wpg_of(kMedSparse, 4)>::value;
+  return waves == 5   ? PoolSize<5, 0, wpg_of(kMedDense, 5)>::value
+         : waves == 6 ? PoolSize<6, 0, wpg_of(kMedDense, 6)>::value
+         : waves == 3 ? PoolSize<3, 0, wpg_of(kMedDense, 3)>::value
+                      : PoolSize<4, 0, wpg_of(kMedDense, 4)>::value;
 }
 
-hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* blocks_per_cu) {
+hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* waves_per_cu) {
   const void* fn = scatter_eps ? wpool_fn<true>(waves, sparse, false) : wpool_fn<false>(waves, sparse, false);
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, fn, 64, 0);
+  int blocks = 0;
+  const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, fn, 64 * wpool_wpg(waves, sparse), 0);
+  *waves_per_cu = blocks * (int)wpool_wpg(waves, sparse);
+  return e;
 }
 
 }  // namespace cvr

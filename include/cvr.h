@@ -156,11 +156,12 @@ typedef enum {
                                  (k_wpair: either wave files into them and runs a batch from them; round
                                  5); 0 (default) one wave per workgroup, private lists.
                                  Scheduling only: results are unchanged. */
-  CVR_OPT_EMPTY_MASK = 28,     /* wave-pool scheduler, sparse media: 1 (default) each wave stages the
-                                 medium's empty-region mask (one bit per super-brick of whole leaves,
-                                 256 bytes) in LDS and loads the brick word of a Woodcock point only
-                                 when its super-brick holds density; 0 loads every point's word.  The
-                                 words it skips are known (0): results are unchanged. */
+  CVR_OPT_EMPTY_MASK = 28,     /* wave-pool scheduler, sparse media: 1 (default) each workgroup (four
+                                 wave-private pools) stages the medium's empty-region mask (one bit per
+                                 super-brick of whole leaves, 256 bytes) in LDS once for its waves, which
+                                 load the brick word of a Woodcock point only when its super-brick holds
+                                 density; 0 loads every point's word.  The words it skips are known
+                                 (0): results are unchanged. */
   /* 21: unused (a drain-time path migration between waves, measured slower: DESIGN.md §6) */
   CVR_OPT_DRAIN = 22,          /* wave-pool scheduler, once the queues are empty: an event batch runs as
                                  soon as the waiting segments x d >= the tracking ones (d = 0: only when

@@ -12,7 +12,7 @@ import pytest
 from parity_util import COUNTERS, assert_pixels_close, oracle_for_scene
 from test_gpu_records import _compare, _ctx
 
-EMASK_BITS = 32 * 64  # kEmaskWords words
+EMASK_BITS = 32 * 64  # kEmaskWords words (cvr_walk.h CVR_WPOOL_EMASK_WORDS)
 
 
 def mask_bits(scene):
@@ -40,7 +40,7 @@ def mask_bits(scene):
 @pytest.mark.parametrize("dims", [(96, 48, 104), (512, 256, 512)])
 def test_mask_has_clear_super_bricks(cvr, dims):
     """The test scenes exercise the skip: clear super-bricks at leaf (es 3) and
-    coarser (es 5) granularity."""
+    coarser (es 5: 32^3 cells) granularity."""
     es, on, n = mask_bits(cvr.Scene.synthetic("cloud", 0, dims))
     assert es == (3 if dims[0] < 128 else 5)
     assert 0 < on < n
