@@ -7,7 +7,7 @@ CPU fallback: on a machine without a GPU, Context() raises.
 from ._lib import (  # noqa: F401
     KERNELS, NAIVE_SK, NAIVE_MK, REGENERATION_SK, STREAMING_MK, STREAMING_SK, SORTING_SK,
     OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS,
-    OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES, OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON, OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT, OPT_FRAME_FLUSH, OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR, OPT_SAMPLE_ORDER, OPT_EMPTY_MASK,
+    OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES, OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON, OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT, OPT_FRAME_FLUSH, OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR, OPT_SAMPLE_ORDER, OPT_EMPTY_MASK, OPT_COUNT_WORDS,
     PATH_RECORD_DTYPE, CvrError, Context, MediumDesc, PinnedImage, Scene, Stats, default_camera, load,
     medium_from_arrays, tile_origin, tiling, write_hdr, LIB_PATH,
 )

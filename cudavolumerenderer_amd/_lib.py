@@ -32,7 +32,7 @@ OPT_MAX_SEGMENTS, OPT_CHUNK, OPT_EVENT_THRESHOLD, OPT_GRID, OPT_SCATTER_EPS = 1,
 OPT_SCHEDULER, OPT_POOL, OPT_TIMING, OPT_CELLS, OPT_WAVES, OPT_ORDER, OPT_QUEUES = 6, 7, 8, 9, 10, 11, 12
 OPT_BOUNDS, OPT_TAIL, OPT_BATCH, OPT_RNG_BINDING, OPT_MORTON = 13, 14, 15, 16, 17
 OPT_WORLD_TO_AABB, OPT_MK_COMPACTION, OPT_SUBQUEUES, OPT_DRAIN, OPT_INFLIGHT, OPT_FRAME_FLUSH = 18, 19, 20, 22, 23, 24
-OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR, OPT_SAMPLE_ORDER, OPT_EMPTY_MASK = 25, 26, 27, 28
+OPT_UNIFORM_ALBEDO, OPT_WAVE_PAIR, OPT_SAMPLE_ORDER, OPT_EMPTY_MASK, OPT_COUNT_WORDS = 25, 26, 27, 28, 29
 
 
 class CvrError(RuntimeError):
@@ -64,7 +64,8 @@ class Stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("steps", C.c_uint64),
                 ("density", C.c_uint64), ("albedo", C.c_uint64), ("escaped", C.c_uint64),
                 ("truncated", C.c_uint64), ("kernel_ms", C.c_double), ("iterations", C.c_uint64),
-                ("track_ms", C.c_double), ("events_ms", C.c_double), ("fetches", C.c_uint64)]
+                ("track_ms", C.c_double), ("events_ms", C.c_double), ("fetches", C.c_uint64),
+                ("words", C.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -145,6 +145,7 @@ struct cvr_ctx {
   int wave_pair = 0;  // CVR_OPT_WAVE_PAIR
   int sample_order = -1;  // CVR_OPT_SAMPLE_ORDER (-1: the default, 0)
   int empty_mask = 1;     // CVR_OPT_EMPTY_MASK
+  int count_words = 0;    // CVR_OPT_COUNT_WORDS
   uint32_t swap_batch = 8;
   int track_grid = 0;
   bool inited = false;
@@ -1267,6 +1268,10 @@ int cvr_set_option(cvr_ctx* c, int opt, int64_t v) {
       if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "empty mask must be 0 or 1");
       c->empty_mask = (int)v;
       return CVR_OK;
+    case CVR_OPT_COUNT_WORDS:
+      if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "count words must be 0 or 1");
+      c->count_words = (int)v;
+      return CVR_OK;
     case CVR_OPT_WAVE_PAIR:
       if (v < 0 || v > 1) return set_err(&c->err, CVR_ERR_INVALID, "wave pair must be 0 or 1");
       if (v == 1 && !cvr::wpool_pair_built())
@@ -1467,7 +1472,7 @@ int cvr_launch_render(cvr_ctx* c) {
       L.frame_done = c->frame_done_active;
     }
     HIP_TRY(c, cvr::launch_wpool(launch_medium(c), L, eps, waves, grid, c->stream, c->wave_pair != 0,
-                                 c->kernel == CVR_KERNEL_NAIVE_MK));
+                                 c->kernel == CVR_KERNEL_NAIVE_MK, c->count_words != 0));
   } else if (L.path_count > 0) {
     if ((r = wf_render(c, L, eps))) return r;
   }
@@ -1541,7 +1546,8 @@ int cvr_image_to_host(const float* device_src, float* host_dst, size_t n_floats,
 int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   if (!c || !st) return set_err(c ? &c->err : nullptr, CVR_ERR_INVALID, "NULL argument");
   HIP_TRY(c, hipStreamSynchronize(c->stream));
-  unsigned long long w[16] = {0};
+  unsigned long long w[32] = {0};  // 16 stats (two rows of 8) and the diagnostic row
+  static_assert(cvr::kStatWordsSlot < 32 && kWorkDebug == kWorkStats + 16 * sizeof(unsigned long long), "work area layout");
   HIP_TRY(c, hipMemcpy(w, c->d_work + kWorkStats, sizeof(w), hipMemcpyDeviceToHost));
   unsigned long long v[8];
   for (int k = 0; k < 8; ++k) v[k] = w[k] + w[8 + k];  // wavefront: events + track rows
@@ -1554,6 +1560,7 @@ int cvr_get_stats(cvr_ctx* c, cvr_stats* st) {
   s.escaped = v[cvr::STAT_ESCAPED];
   s.truncated = v[cvr::STAT_TRUNCATED];
   s.fetches = v[cvr::STAT_FETCH];
+  s.words = w[cvr::kStatWordsSlot];  // counting launches only (CVR_OPT_COUNT_WORDS)
   s.kernel_ms = 0.0;
   if (c->timed) {
     float ms = 0.f;
@@ -1722,6 +1729,7 @@ int cvr_render_tiles(cvr_ctx* c, const cvr_render_desc* d, uint32_t first_tile, 
     acc.escaped += s.escaped;
     acc.truncated += s.truncated;
     acc.fetches += s.fetches;
+    acc.words += s.words;
     acc.kernel_ms += s.kernel_ms;
     if ((r = cvr_reset(c))) goto done;  // prepareForNextIterations
     if (ntiles != 1 && (r = cvr_clear_output(c))) goto done;
@@ -1845,6 +1853,7 @@ static void copy_settings(cvr_ctx* d, const cvr_ctx* s) {
   d->drain = s->drain;
   d->sample_order = s->sample_order;
   d->empty_mask = s->empty_mask;
+  d->count_words = s->count_words;
   d->order = s->order;
   d->max_segments = s->max_segments;
   d->chunk = s->chunk;
@@ -2056,6 +2065,7 @@ int cvr_render_frame(cvr_ctx* c, float* host_image, size_t host_floats, uint32_t
     acc.escaped += s.escaped;
     acc.truncated += s.truncated;
     acc.fetches += s.fetches;
+    acc.words += s.words;
   }
   float ms = 0.f;  // clear to the end of the band that ends last
   for (uint32_t k = 0; k < parts; ++k) {

@@ -57,8 +57,9 @@ bool wpool_pair_built();
 // pair: two waves per workgroup sharing their event lists (k_wpair; dense media with
 // cells and bounds, 5 waves per SIMD, no records / in-launch output; else k_wpool).
 // naive_mk: naiveMK's walk on the wave pool (5 waves per SIMD, no records / in-launch output).
+// count_words: sparse media, the counting instance (CVR_OPT_COUNT_WORDS: brick words loaded).
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
-                        hipStream_t s, bool pair = false, bool naive_mk = false);
+                        hipStream_t s, bool pair = false, bool naive_mk = false, bool count_words = false);
 // Resident waves per CU of the wave-pool instance (workgroups per CU x waves per workgroup).
 hipError_t wpool_occupancy(bool scatter_eps, int waves, bool sparse, int* waves_per_cu);
 // Pool slots per wave of the wave-pool kernel instance (LaunchParams::pool_T

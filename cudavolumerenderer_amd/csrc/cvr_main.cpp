@@ -388,6 +388,7 @@ int main(int argc, char** argv) {
         st.escaped += sts[k].escaped;
         st.truncated += sts[k].truncated;
         st.fetches += sts[k].fetches;
+        st.words += sts[k].words;
         st.iterations += sts[k].iterations;
         st.track_ms += sts[k].track_ms;
         st.events_ms += sts[k].events_ms;

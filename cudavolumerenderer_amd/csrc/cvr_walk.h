@@ -193,6 +193,9 @@ struct MediumParams {
 #define CVR_WPOOL_EMASK_WORDS 64
 #endif
 constexpr int kEmaskWords = CVR_WPOOL_EMASK_WORDS;
+// u64 index in the work area's counters (the diagnostic row, cvr_kernels.h kWorkDebug)
+// of the brick words a counting launch loaded (CVR_OPT_COUNT_WORDS, cvr_stats.words)
+constexpr uint32_t kStatWordsSlot = 24;
 static_assert(kEmaskWords >= 64 && (kEmaskWords & (kEmaskWords - 1)) == 0, "mask words: a power of two >= 64");
 
 // Brick-bound code -> bound (MediumParams::bounds): the float with bits
@@ -564,8 +567,10 @@ CVR_DEV WoodcockPoint woodcock_point(const MediumParams& m, V3 o, V3 d, float t)
 // pointer; the brick word is loaded only when the point's super-brick has a
 // cell leaf: in a clear one it is 0 (bound code 0, the zero cell leaf), and off
 // the grid the sentinel's (255 << 24, slot 0), both known without a load.
+// n_words (counting instances only, CVR_OPT_COUNT_WORDS): += 1 per brick word loaded.
 template <int kWords, class EmWords>
-CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float t, const EmWords& em) {
+CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float t, const EmWords& em,
+                                        uint32_t* n_words = nullptr) {
   WoodcockPoint P;
   woodcock_coords(m, o, d, t, P);
   const uint32_t x1 = (uint32_t)P.cx, y1 = (uint32_t)P.cy, z1 = (uint32_t)P.cz;
@@ -576,6 +581,7 @@ CVR_DEV WoodcockPoint woodcock_point_em(const MediumParams& m, V3 o, V3 d, float
   const bool load = P.in & (__builtin_amdgcn_ubfe(word, sb & 31u, 1u) != 0u);
   uint32_t sw = P.in ? 0u : 255u << 24;
   if (load) sw = m.sbounds[__umul24(z1 >> m.bshift, m.bnxy) + __umul24(y1 >> m.bshift, m.bnx) + (x1 >> m.bshift)];
+  if (n_words) *n_words += load ? 1u : 0u;
   P.qb = bound_value(sw >> 24);
   P.cp = m.cells + ((((size_t)(sw & 0xFFFFFFu)) << 9 | leaf_local(x1, y1, z1)) << 1);
   return P;

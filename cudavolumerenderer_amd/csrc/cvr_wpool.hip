@@ -616,9 +616,15 @@ __device__ unsigned long long g_tail[8 * kTailWaves];
 // the RNG re-seeded from (iteration, pixel, depth) and three unused draws; the slot's
 // event-only word holds the path id (iteration and pixel) instead of the pixel.
 constexpr int kMedMK = 4;
+// kMedCount (or-ed into kMed, sparse media only): the counting instance of
+// CVR_OPT_COUNT_WORDS, which also counts the brick words its Woodcock points load
+// (the empty-region mask skips the rest), so that the launch's algorithmic bytes are
+// exact; the benchmarked instances carry no counter.
+constexpr int kMedCount = 8;
 template <bool kScatterEps, int kWaves, int kMedMk, bool kRecord, bool kFlush>
 __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(MediumParams mk, LaunchParams Lk) {
   constexpr bool kMK = (kMedMk & kMedMK) != 0;
+  constexpr bool kCountWords = (kMedMk & kMedCount) != 0;
   constexpr int kMed = kMedMk & 3;
   static_assert(!kMK || (kScatterEps && !kRecord && !kFlush), "naiveMK: scatter -eps, no records / in-launch output");
   constexpr bool kSparse = kMed == kMedSparse;
@@ -697,6 +703,7 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
   // pool's LDS counters once per batch (no per-lane registers, no SGPRs, live
   // across the track loop); the track loop counts steps and fetches per lane.
   uint32_t c_steps = 0, c_fetch = 0;
+  uint32_t c_words = 0;  // kCountWords: brick words loaded
   if (lane < (uint32_t)STAT_COUNT) S.cnt[lane] = 0u;
   if (lane == 0) {
     S.dead = 0ull;
@@ -836,7 +843,7 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
 #pragma unroll
           for (int k = 0; k < kLook; ++k) {
             if constexpr (kEm != 0)
-              Pk[k] = woodcock_point_em<kEm>(m, o, d, tk[k], EM);
+              Pk[k] = woodcock_point_em<kEm>(m, o, d, tk[k], EM, kCountWords ? &c_words : nullptr);
             else
               Pk[k] = woodcock_point(m, o, d, tk[k]);
           }
@@ -1265,6 +1272,12 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
                                               S.cnt[STAT_ALBEDO], S.cnt[STAT_ESCAPED], S.cnt[STAT_TRUNCATED], fetch};
     if (lane < (uint32_t)STAT_COUNT && w[lane])
       __hip_atomic_fetch_add(gmem(L.stats + lane), w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (kCountWords) {
+      unsigned long long words = c_words;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) words += __shfl_xor(words, off);
+      if (lane == 0) __hip_atomic_fetch_add(gmem(L.stats + kStatWordsSlot), words, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1818,7 +1831,7 @@ static const void* wpool_mk_fn(bool sparse, bool full, bool uniform) {
 }
 
 hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatter_eps, int waves, uint32_t grid,
-                        hipStream_t s, bool pair, bool naive_mk) {
+                        hipStream_t s, bool pair, bool naive_mk, bool count_words) {
   if (L.path_count == 0) return hipSuccess;
   const bool sparse = m.leaves != nullptr;
   const bool flush = L.frame_done != nullptr;
@@ -1852,6 +1865,11 @@ hipError_t launch_wpool(const MediumParams& m, const LaunchParams& L, bool scatt
   const void* fn = L.rec ? (scatter_eps ? wpool_record_fn<true>(waves, sparse) : wpool_record_fn<false>(waves, sparse))
                          : (scatter_eps ? wpool_fn<true>(waves, sparse, full, flush, uniform)
                                         : wpool_fn<false>(waves, sparse, full, flush, uniform));
+  // the counting instances (CVR_OPT_COUNT_WORDS): sparse media, 5 waves per SIMD, no records
+  // or in-launch output (other launches count nothing: cvr_stats.words stays 0)
+  if (count_words && sparse && waves == 5 && !L.rec && !flush)
+    fn = scatter_eps ? reinterpret_cast<const void*>(&k_wpool<true, 5, kMedSparse | kMedCount, false, false>)
+                     : reinterpret_cast<const void*>(&k_wpool<false, 5, kMedSparse | kMedCount, false, false>);
   if (!fn) return hipErrorInvalidValue;  // no record / in-launch output instance for this register budget
   // (a grid of whole workgroups: pool_T and the record ids are sized for grid waves)
   if (grid % wpool_wpg(waves, sparse)) return hipErrorInvalidValue;

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define CVR_ABI_VERSION 3  /* 3: cvr_render_frame takes the host buffer size */
+#define CVR_ABI_VERSION 4  /* 3: cvr_render_frame takes the host buffer size; 4: cvr_stats.words */
 
 enum {
   CVR_OK = 0,
@@ -162,6 +162,11 @@ typedef enum {
                                  load the brick word of a Woodcock point only when its super-brick holds
                                  density; 0 loads every point's word.  The words it skips are known
                                  (0): results are unchanged. */
+  CVR_OPT_COUNT_WORDS = 29,    /* wave-pool scheduler, sparse media, 5 waves per SIMD: 1 runs the counting
+                                 instance, which also counts the brick words its Woodcock points load
+                                 into cvr_stats.words (the benchmark's exact algorithmic bytes; one
+                                 more VGPR in the track loop, so not the benchmarked kernel); 0
+                                 (default) counts nothing.  Results are unchanged. */
   /* 21: unused (a drain-time path migration between waves, measured slower: DESIGN.md §6) */
   CVR_OPT_DRAIN = 22,          /* wave-pool scheduler, once the queues are empty: an event batch runs as
                                  soon as the waiting segments x d >= the tracking ones (d = 0: only when
@@ -229,6 +234,8 @@ typedef struct cvr_stats {
   double track_ms;     /* wavefront: summed device time of the tracking kernels (CVR_OPT_TIMING) */
   double events_ms;    /* wavefront: summed device time of the event kernels (CVR_OPT_TIMING) */
   uint64_t fetches;    /* density cells fetched (evaluations not settled by a brick bound) */
+  uint64_t words;      /* sparse media: brick words loaded (the empty-region mask skips the
+                          rest); counted only by launches with CVR_OPT_COUNT_WORDS 1, else 0 */
 } cvr_stats;
 
 typedef struct cvr_path_record {
