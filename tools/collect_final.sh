@@ -4,13 +4,13 @@
 set -eu
 cd "$(dirname "$0")/.."
 F=gpurun_out/final
-P=${1:-profiles/round5}
+P=${1:-profiles/round6}
 for sc in manix hetvol cloud; do
   case $sc in manix) key=k_wpool_1024x1024_20it; c=c2;; hetvol) key=hetvol_k_wpool_1024x1024_20it; c=c3;;
                      cloud) key=cloud_k_wpool_4096x4096_20it; c=c5;; esac
-  python3 tools/traffic.py $F/pmcf_$sc $F/pmcw_$sc $key | cut -c1-140
   case $sc in manix) inst="k_wpool<false, 5, 2, false, false>";; hetvol) inst="k_wpool<false, 5, 3, false, false>";;
               cloud) inst="k_wpool<false, 5, 1, false, false>";; esac
+  python3 tools/traffic.py $F/pmcf_$sc $F/pmcw_$sc $key "$inst" | cut -c1-140
   python3 tools/valu.py $F/pmcv_$sc $key "$inst" | cut -c1-140
   cp $F/prof_$sc/run_kernel_stats.csv $P/${c}_kernel_stats.csv
   if [ $sc = cloud ]; then sw="3 1"; else sw="20 5"; fi

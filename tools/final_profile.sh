@@ -30,16 +30,17 @@ for sc in manix hetvol cloud; do
   if [ $sc = cloud ]; then S="--steps 3 --warmup 1"; else S="--steps 20 --warmup 5"; fi
   step prof_$sc 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$sc" -o run --output-format csv -- $B --no-shard-emulation --scene $sc $S
   if [ $sc = cloud ]; then S="--steps 2 --warmup 1"; else S="--steps 3 --warmup 1"; fi
-  step pmcf_$sc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
-  step pmcw_$sc 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
-  step pmcv_$sc 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- $B --scene $sc --serial $S
+  # (--no-count-words: no counting launch of a sparse medium, so only the benchmarked instance runs)
+  step pmcf_$sc 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmcf_$sc" -o run --output-format csv -- $B --scene $sc --serial --no-count-words $S
+  step pmcw_$sc 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmcw_$sc" -o run --output-format csv -- $B --scene $sc --serial --no-count-words $S
+  step pmcv_$sc 400 rocprofv3 --pmc SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcv_$sc" -o run --output-format csv -- $B --scene $sc --serial --no-count-words $S
   cp "$OUT/libcvr.sha256" "$OUT/pmcf_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcw_$sc/"; cp "$OUT/libcvr.sha256" "$OUT/pmcv_$sc/"
 done
 # fold the traffic passes into profiles/traffic.json here too, so the bench lines
 # below (same libcvr.so) carry their measured traffic
-python3 tools/traffic.py "$OUT/pmcf_manix" "$OUT/pmcw_manix" k_wpool_1024x1024_20it > /dev/null &&
-  python3 tools/traffic.py "$OUT/pmcf_hetvol" "$OUT/pmcw_hetvol" hetvol_k_wpool_1024x1024_20it > /dev/null &&
-  python3 tools/traffic.py "$OUT/pmcf_cloud" "$OUT/pmcw_cloud" cloud_k_wpool_4096x4096_20it > /dev/null || exit 1
+python3 tools/traffic.py "$OUT/pmcf_manix" "$OUT/pmcw_manix" k_wpool_1024x1024_20it "k_wpool<false, 5, 2, false, false>" > /dev/null &&
+  python3 tools/traffic.py "$OUT/pmcf_hetvol" "$OUT/pmcw_hetvol" hetvol_k_wpool_1024x1024_20it "k_wpool<false, 5, 3, false, false>" > /dev/null &&
+  python3 tools/traffic.py "$OUT/pmcf_cloud" "$OUT/pmcw_cloud" cloud_k_wpool_4096x4096_20it "k_wpool<false, 5, 1, false, false>" > /dev/null || exit 1
 # and the VALU issue (roofline.valu) of each benchmark kernel instance
 python3 tools/valu.py "$OUT/pmcv_manix" k_wpool_1024x1024_20it "k_wpool<false, 5, 2, false, false>" > /dev/null &&
   python3 tools/valu.py "$OUT/pmcv_hetvol" hetvol_k_wpool_1024x1024_20it "k_wpool<false, 5, 3, false, false>" > /dev/null &&
@@ -55,15 +56,12 @@ step pmc_a 200 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_AN
 step pmc_b 200 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc_b" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
 step pmc_c 200 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc_c" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
 step pmc_d 200 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_IFETCH SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_LDS_BANK_CONFLICT --kernel-trace -d "$OUT/pmc_d" -o run --output-format csv -- $B --serial --steps 3 --warmup 1
-C5="$B --scene cloud --serial --steps 2 --warmup 1"
+C5="$B --scene cloud --serial --no-count-words --steps 2 --warmup 1"
 step pmc5_a 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU --kernel-trace -d "$OUT/pmc5_a" -o run --output-format csv -- $C5
 step pmc5_b 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_TA_BUSY --kernel-trace -d "$OUT/pmc5_b" -o run --output-format csv -- $C5
 step pmc5_c 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum --kernel-trace -d "$OUT/pmc5_c" -o run --output-format csv -- $C5
-# round 5: every kernel id's C2 line (all on the wave pool by default), and the paired-wave
-# variant (CVR_OPT_WAVE_PAIR) against the one-wave pool with the lane-fill counters
+# every kernel id's C2 line (all on the wave pool by default)
 for k in streamingSK sortingSK streamingMK naiveSK naiveMK; do
   step k_$k 300 python3 bench.py --kernel $k --steps 20 --warmup 5 --no-shard-emulation --no-cpu-baseline
 done
-step pair_pmc 400 bash tools/pmc_tune.sh "SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" manix,hetvol one=regenerationSK: pair=regenerationSK:pair=1
-step pair_time 300 python3 tools/tune.py --scene manix --rounds 4 --variants regenerationSK: regenerationSK:pair=1
 echo "final profile done"
