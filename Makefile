@@ -68,3 +68,7 @@ variant: $(SRCS_HIP) $(SRCS_CPP) $(HDRS)
 variant-pair:
 	$(MAKE) variant NAME=pair DEFS="-DCVR_WPOOL_PAIR=1"
 .PHONY: variant-pair
+# Cell fetches as track-ready work (round-6 experiment, measured slower: profiles/round6/ab/fetch_list/)
+variant-fetchlist:
+	$(MAKE) variant NAME=fetchlist DEFS="-DCVR_WPOOL_FETCH_LIST=1"
+.PHONY: variant-fetchlist

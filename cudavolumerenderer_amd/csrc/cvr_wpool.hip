@@ -79,6 +79,17 @@
 #ifndef CVR_WPOOL_LOOK
 #define CVR_WPOOL_LOOK 2
 #endif
+// Cell fetches as track-ready work (round-6 experiment, dense instances with cells and
+// bounds; 0: off, the default and the only form in libcvr.so).  A point the brick bound
+// does not settle ends the lane's turn: the path's (t, rng) go back to the pool and its slot
+// joins the track-ready ring marked "fetch pending" (bit 7 of the ring entry); the lanes
+// that pull marked entries at a swap fetch their cells together and either file a
+// collision or track on, so no lane idles for another lane's cell and the two per-group
+// fetch blocks of the track loop (~5% lane fill) go away.  The same points and draws: the
+// test value is the path's last draw, re-derived from the stored XORWOW state.
+#ifndef CVR_WPOOL_FETCH_LIST
+#define CVR_WPOOL_FETCH_LIST 0
+#endif
 constexpr int kLook = CVR_WPOOL_LOOK;
 // The track loop runs CVR_WPOOL_UNROLL / kLook groups: a variant build with
 // UNROLL < kLook would run none (tracking lanes never step: the launch never
@@ -631,6 +642,7 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
   // Sparse media defer their cell fetches to the end of the track iteration
   // (the lookahead below): C5 -3.0%; the dense instances lose 5-8% with it.
   constexpr bool kLookDefer = kSparse && CVR_WPOOL_SPARSE_DEFER;
+  constexpr bool kFetchList = CVR_WPOOL_FETCH_LIST && !kMK && (kMed == kMedDenseFull || kMed == kMedDenseFullUniform);
   // (dense media: +7% C2, +6% C3 with a 16-word mask)
   constexpr int kEm = kSparse && CVR_WPOOL_EMASK ? kEmaskWords : 0;
   // waves per workgroup, each with a pool of its own (kWpgSparse on sparse media)
@@ -678,6 +690,7 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
                     (size_t)PoolSize<kWaves, 0, kWpg>::kBudget,
                 "wave pools exceed the LDS budget of kWaves waves per SIMD");
   static_assert(kSlots <= 256, "the pool's rings and stacks hold slot indices as uint8_t");
+  static_assert(!kFetchList || kSlots <= 128, "fetch-pending ring entries carry bit 7");
   __shared__ WavePool<kSlots> Sw[kWpg];
   WavePool<kSlots>& S = Sw[wv];
   // the empty-region mask (sparse media), one copy per workgroup
@@ -768,24 +781,46 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
         n_lc += (uint32_t)__popcll(mc);
         n_lb += (uint32_t)__popcll(mb);
         n_over += (uint32_t)__popcll(__ballot(fst == 1));
+        if constexpr (kFetchList) {  // fetch pending: back to the ready ring, marked
+          const unsigned long long mf = __ballot(fst == 4);
+          if (fst == 4) S.ready[(ready_head + n_ready + lane_rank(mf)) % kSlots] = (uint8_t)(slot | 0x80);
+          n_ready += (uint32_t)__popcll(mf);
+        }
         if (fst != 0) {
           slot = -1;
           fst = 0;
         }
         const unsigned long long idle = __ballot(slot < 0);
         const uint32_t k = min((uint32_t)__popcll(idle), n_ready), rank = lane_rank(idle);
+        bool pend = false;
         if (slot < 0 && rank < k) {
           const uint32_t r = ready_head + rank;
-          const uint32_t s = S.ready[r >= (uint32_t)kSlots ? r - kSlots : r];
+          uint32_t s = S.ready[r >= (uint32_t)kSlots ? r - kSlots : r];
+          if constexpr (kFetchList) {
+            pend = (s & 0x80u) != 0u;
+            s &= 0x7Fu;
+          }
           slot = (int)s;
           load_track(S, s, o, d, rng, t, max_t);
         }
         ready_head += k;
         if (ready_head >= (uint32_t)kSlots) ready_head -= kSlots;
         n_ready -= k;
+        if constexpr (kFetchList) {
+          if (pend) {  // the pending point's cell, fetched by every lane that pulled one
+            ++c_fetch;
+            WoodcockPoint P;
+            woodcock_coords(m, o, d, t, P);
+            const uint32_t x1 = (uint32_t)P.cx, y1 = (uint32_t)P.cy, z1 = (uint32_t)P.cz;
+            P.cp = m.cells + 2 * (__umul24(z1, m.rxy) + __umul24(y1, m.rx) + x1);
+            const float xt = det_fmaf((float)(rng.v4 + rng.d), 2.3283064e-10f, 1.1641532e-10f);  // its test draw
+            const float rho = m.scale * woodcock_density(m, P);
+            fst = !(rho * m.inv_sigma < xt) ? 2 : 0;
+          }
+        }
       }
       const uint32_t n_act = (uint32_t)__popcll((__ballot(slot >= 0) & __ballot(fst == 0)));
-      const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0));
+      const uint32_t n_fin = (uint32_t)__popcll(__ballot(fst != 0 && (!kFetchList || fst != 4)));
       // EVENT next: a full wave of waiting events, slots never filled, or
       // nothing left to track.  Park: tracking lanes return (t, rng) to the
       // pool, finished lanes are filed.  (Once the queues are empty n_ln is a
@@ -793,9 +828,10 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
       if (n_lb + n_lc + n_ln + n_fin >= 64u || (n_act == 0u && n_ready == 0u)) {
         if (fst == 2 && !(t < max_t)) fst = 3;
         if (slot >= 0) store_track(S, (uint32_t)slot, t, rng);
-        const unsigned long long mr = (__ballot(slot >= 0) & __ballot(fst == 0));
+        const unsigned long long mr = (__ballot(slot >= 0) & __ballot(fst == 0 || (kFetchList && fst == 4)));
         const unsigned long long mc = __ballot(fst == 2), mb = __ballot(fst & 1);
-        if (slot >= 0 && fst == 0) S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)slot;
+        if (slot >= 0 && (fst == 0 || (kFetchList && fst == 4)))
+          S.ready[(ready_head + n_ready + lane_rank(mr)) % kSlots] = (uint8_t)(slot | (fst == 4 ? 0x80 : 0));
         if (fst == 2) S.lc[n_lc + lane_rank(mc)] = (uint8_t)slot;
         if (fst & 1) S.lb[n_lb + lane_rank(mb)] = (uint8_t)slot;
         n_over += (uint32_t)__popcll(__ballot(fst == 1));
@@ -860,6 +896,9 @@ __global__ __launch_bounds__(64 * wpg_of(kMedMk, kWaves), kWaves) void k_wpool(M
                   end = k;
                   pcp = Pk[k].cp;
                   pxt = xtk[k];
+                } else if constexpr (kFetchList) {
+                  fst = 4;  // cell fetch pending: filed as marked track-ready work at the next swap
+                  end = k;
                 } else {
                   ++c_fetch;
                   const float rho = m.scale * woodcock_density(m, Pk[k]);
