@@ -64,7 +64,8 @@ typedef enum {
   CVR_OPT_CHUNK = 2,          /* paths per wave dequeue (persistent schedulers); 0 (default): 256, the
                                  wave pool 64..256 by the paths each of its waves gets */
   CVR_OPT_EVENT_THRESHOLD = 3,/* lanes per wave that must wait before events run */
-  CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy) */
+  CVR_OPT_GRID = 4,           /* persistent grid size in blocks (0 = occupancy); for the wave-pool scheduler in
+                                 waves, rounded down to whole workgroups (four waves on sparse media) */
   CVR_OPT_SCATTER_EPS = 5,    /* -1 kernel default, 0 off, 1 on */
   CVR_OPT_SCHEDULER = 6,      /* how paths map onto threads: 0 single persistent kernel, 1 wavefront
                                  pair (streamingMK's multi-kernel structure), 2 workgroup path pool
