@@ -61,19 +61,28 @@ static inline f3 normalize3(f3 v) { return scl3(v, 1.0f / det_sqrtf(dot3(v, v)))
  * curand_uniform).  Third-party (CUDA Toolkit 12.0, not vendored). */
 typedef struct { uint32_t v[5]; uint32_t d; } xorwow_t;
 
-static inline void rng_init(xorwow_t* s, int32_t seed) {
-  /* Rng(int seed) -> curand_init(unsigned long long): sign extension (Q3) */
-  unsigned long long sd = (unsigned long long)(long long)seed;
-  uint32_t s0 = ((uint32_t)sd) ^ 0xaad26b49u;
-  uint32_t s1 = ((uint32_t)(sd >> 32)) ^ 0xf7dcefddu;
-  uint32_t t0 = 1099087573u * s0;
-  uint32_t t1 = 2591861531u * s1;
+/* The seeding structure (which scrambled seed words add / xor into which state
+ * words, and the Weyl counter's start), with the generator's four scramble
+ * constants as parameters: cuRAND's below; oracle_rng_state_consts runs it with
+ * rocRAND's, whose xorwow_engine seeds with the same structure, so that structure
+ * is pinned against an independent implementation (tests/test_oracle_cpu.py) and
+ * only cuRAND's four constants are restated from the CUDA headers. */
+static inline void rng_init_consts(xorwow_t* s, unsigned long long sd, uint32_t x0, uint32_t x1, uint32_t m0,
+                                   uint32_t m1) {
+  uint32_t s0 = ((uint32_t)sd) ^ x0;
+  uint32_t s1 = ((uint32_t)(sd >> 32)) ^ x1;
+  uint32_t t0 = m0 * s0;
+  uint32_t t1 = m1 * s1;
   s->d = 6615241u + t1 + t0;
   s->v[0] = 123456789u + t0;
   s->v[1] = 362436069u ^ t0;
   s->v[2] = 521288629u + t1;
   s->v[3] = 88675123u ^ t1;
   s->v[4] = 5783321u + t0;
+}
+static inline void rng_init(xorwow_t* s, int32_t seed) {
+  /* Rng(int seed) -> curand_init(unsigned long long): sign extension (Q3) */
+  rng_init_consts(s, (unsigned long long)(long long)seed, 0xaad26b49u, 0xf7dcefddu, 1099087573u, 2591861531u);
 }
 static inline uint32_t rng_next(xorwow_t* s) {
   uint32_t t = s->v[0] ^ (s->v[0] >> 2);
@@ -1289,6 +1298,14 @@ EXPORT void oracle_rng_stream(int32_t seed, uint32_t n, uint32_t* out_u32, float
 EXPORT void oracle_rng_state(int32_t seed, uint32_t out[6]) {
   xorwow_t s;
   rng_init(&s, seed);
+  memcpy(out, s.v, 5 * sizeof(uint32_t));
+  out[5] = s.d;
+}
+/* The seeding structure with other scramble constants (the rocRAND pin). */
+EXPORT void oracle_rng_state_consts(unsigned long long seed, uint32_t x0, uint32_t x1, uint32_t m0, uint32_t m1,
+                                    uint32_t out[6]) {
+  xorwow_t s;
+  rng_init_consts(&s, seed, x0, x1, m0, m1);
   memcpy(out, s.v, 5 * sizeof(uint32_t));
   out[5] = s.d;
 }

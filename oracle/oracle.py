@@ -83,6 +83,7 @@ def load():
     lib.oracle_render_mk_reference.restype = C.c_int
     lib.oracle_rng_stream.argtypes = [C.c_int32, C.c_uint32, P, P]
     lib.oracle_rng_state.argtypes = [C.c_int32, P]
+    lib.oracle_rng_state_consts.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P]
     lib.oracle_density.argtypes = [C.POINTER(OracleMedium), P]
     lib.oracle_density.restype = C.c_float
     lib.oracle_aabb.argtypes = [C.POINTER(OracleMedium), P, P, P]
@@ -263,6 +264,14 @@ def rng_state(seed: int):
     lib = load()
     s = np.zeros(6, np.uint32)
     lib.oracle_rng_state(seed, _p(s))
+    return s
+
+
+def rng_state_consts(seed: int, x0: int, x1: int, m0: int, m1: int):
+    """The oracle's seeding structure with other scramble constants (rng_init_consts)."""
+    lib = load()
+    s = np.zeros(6, np.uint32)
+    lib.oracle_rng_state_consts(seed & 0xFFFFFFFFFFFFFFFF, x0, x1, m0, m1, _p(s))
     return s
 
 

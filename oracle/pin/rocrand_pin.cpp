@@ -10,10 +10,13 @@
 // implementation (tests/test_oracle_cpu.py).
 //
 //   rocrand_pin v0 v1 v2 v3 v4 d n   -> n decimal u32 values, one per line
+//   rocrand_pin seed S               -> rocRAND's state after xorwow_engine(S, 0, 0): v0..v4 d
+//                                       (pins the oracle's seeding structure, rng_init_consts)
 #include <rocrand/rocrand_xorwow.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 struct pinned_xorwow : rocrand_device::xorwow_engine {
   pinned_xorwow(const unsigned (&v)[5], unsigned d) : xorwow_engine(0ull, 0ull, 0ull) {
@@ -22,7 +25,19 @@ struct pinned_xorwow : rocrand_device::xorwow_engine {
   }
 };
 
+struct seeded_xorwow : rocrand_device::xorwow_engine {
+  explicit seeded_xorwow(unsigned long long seed) : xorwow_engine(seed, 0ull, 0ull) {}
+  void print() const {
+    for (int i = 0; i < 5; ++i) std::printf("%u\n", m_state.x[i]);
+    std::printf("%u\n", m_state.d);
+  }
+};
+
 int main(int argc, char** argv) {
+  if (argc == 3 && std::string(argv[1]) == "seed") {
+    seeded_xorwow(std::strtoull(argv[2], nullptr, 10)).print();
+    return 0;
+  }
   if (argc != 8) {
     std::fprintf(stderr, "usage: %s v0 v1 v2 v3 v4 d n\n", argv[0]);
     return 2;

@@ -103,6 +103,22 @@ def test_rng_next_matches_rocrand_xorwow(oracle_mod, seed):
     assert np.array_equal(u, ref)
 
 
+@pytest.mark.parametrize("seed", [0, 1, 12345, 2 ** 31 - 1, 2 ** 32 + 7, 2 ** 64 - 1])
+def test_rng_seeding_structure_matches_rocrand(oracle_mod, seed):
+    """Pin: the oracle's seeding structure (rng_init_consts: which scrambled seed
+    words add / xor into which state words, the Weyl counter's start) run with
+    rocRAND's four scramble constants equals rocRAND's xorwow_engine(seed, 0, 0)
+    state, an independent implementation of the same seeding; only cuRAND's four
+    constants (0xaad26b49, 0xf7dcefdd, 1099087573, 2591861531) stay restated from
+    the CUDA headers."""
+    if not os.path.exists(PIN):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+    out = subprocess.check_output([PIN, "seed", str(seed)], text=True)
+    ref = [int(v) for v in out.split()]
+    got = [int(v) for v in oracle_mod.rng_state_consts(seed, 0x2c7f967f, 0xa03697cb, 1228688033, 2073658381)]
+    assert got == ref
+
+
 def test_rng_uniform_mapping(oracle_mod):
     """curand_uniform = x * 2^-32 + 2^-33 as one fp32 FMA: in (0, 1], and
     equal to the float64 value rounded once."""
