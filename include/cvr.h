@@ -155,8 +155,10 @@ typedef enum {
   CVR_OPT_WAVE_PAIR = 26,      /* wave-pool scheduler, dense media with cells and bounds: 1 runs two waves
                                  per workgroup whose boundary and collision event lists are shared
                                  (k_wpair: either wave files into them and runs a batch from them; round
-                                 5); 0 (default) one wave per workgroup, private lists.
-                                 Scheduling only: results are unchanged. */
+                                 5, 4.1x slower: profiles/round5/README.md); 0 (default) one wave per
+                                 workgroup, private lists.  Only `make variant-pair` builds k_wpair: the
+                                 in-tree libcvr.so refuses 1 with CVR_ERR_UNSUPPORTED.  Scheduling only:
+                                 results are unchanged. */
   CVR_OPT_EMPTY_MASK = 28,     /* wave-pool scheduler, sparse media: 1 (default) each workgroup (four
                                  wave-private pools) stages the medium's empty-region mask (one bit per
                                  super-brick of whole leaves, 256 bytes) in LDS once for its waves, which
