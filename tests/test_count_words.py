@@ -50,3 +50,26 @@ def test_dense_media_count_nothing(cvr):
     _, st = c.render_image(64, 64, (1, 1), 2)
     c.close()
     assert st.words == 0 and st.density > 0
+
+
+@pytest.mark.gpu
+def test_bench_line_counts_sparse_words(tmp_path):
+    """bench.py on a sparse scene reports the words its counting launch found
+    (counts_per_launch.brick_words_loaded) and builds its algorithmic bytes from
+    them, so the bytes are exact rather than one word per density evaluation."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--scene", "cloud", "--resolution", "256", "256",
+                        "--iterations", "2", "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                        "--no-shard-emulation"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    roof = line["roofline"]
+    counts = roof["counts_per_launch"]
+    words = counts["brick_words_loaded"]
+    assert 0 < words < counts["density_evals"]
+    # 32 B per fetched cell + 4 B per word + 12 B per escape (the cloud's albedo is a constant)
+    assert roof["algorithmic_bytes_per_launch"] == 32 * counts["cell_fetches"] + 4 * words + 12 * counts["escaped"]
